@@ -1,0 +1,151 @@
+/*
+ * scion_hfv.h -- C ABI of libscionhfv.so: SCION border-router hop-field (HF) AES-CMAC
+ * verification on AMD MI355X (gfx950).
+ *
+ * What it replaces in the reference (netsys-lab/scion-xdp-br):
+ *   - the per-packet data-plane call  int verify_hop_field(struct macinput*, u64 expected)
+ *     (br/src/bpf/xdp.c:77-91) together with the macinput assembly and beta/SegID rule of
+ *     defer_verify_hop_field / scion_as_ingress (br/src/bpf/path_processing.h:39-81),
+ *     now executed for a whole batch per kernel launch;
+ *   - the control-plane key table  mac_key_map  (br/src/bpf/maps.h:60-67) and its writers
+ *     `br-loader key add|remove` (br/src/br_loader.cpp:182-261).
+ *
+ * Conventions
+ *   - Status: 0 on success, a negative errno on failure (-EINVAL bad argument, -ENODEV no
+ *     usable GPU, -ENOMEM allocation, -EIO HIP runtime error).  hfv_last_error() returns a
+ *     human-readable message for the calling thread.  No C++ exception crosses the ABI.
+ *   - Batch buffers (records, macinputs, tags, pass bitmaps) are DEVICE pointers (hipMalloc,
+ *     hipMallocManaged or a framework allocation on the ctx's GPU) unless a function says
+ *     otherwise.  `stream` is a hipStream_t passed as void*; NULL selects the ctx's own
+ *     stream.  Calls enqueue work and return; completion is stream-ordered.
+ *   - Verdict output: bit (i % 64) of pass_bits[i / 64] is 1 iff packet i's hop field
+ *     verifies; bits for i >= n in the last word are 0.  A missing key fails closed
+ *     (xdp.c:83-84).
+ *   - Threading: one ctx per GPU, used by one host thread at a time (or externally
+ *     serialised), like one XDP program instance per CPU queue.
+ */
+#ifndef SCION_HFV_H
+#define SCION_HFV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hfv_aes.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HFV_ABI_VERSION 1
+#define HFV_MAX_KEYS 256          /* key slots; the reference map holds 8 (maps.h:60-67) */
+#define HFV_REC_INF_OFF 40        /* default 64 B record layout, DESIGN.md section 3 */
+#define HFV_REC_HF_OFF 48
+
+/* struct macinput (include/bpf/scion.h:122-132): 16 B, wire byte order */
+struct macinput {
+    uint16_t null0;
+    uint16_t beta;
+    uint32_t ts;
+    uint8_t null1;
+    uint8_t exp;
+    uint16_t ingress;
+    uint16_t egress;
+    uint16_t null2;
+} __attribute__((packed));
+
+/* struct hop_key (br/src/bpf/common.h:87-91): expanded key + CMAC subkey K1, 192 B */
+struct hop_key {
+    struct aes_key_schedule key;
+    struct aes_block subkey;
+};
+
+/* Per-packet key selection (SURVEY.md 8b iii) */
+enum hfv_keysel {
+    HFV_KEYSEL_ZERO = 0,  /* mac_key_map[0] for every packet: the reference rule, xdp.c:82 */
+    HFV_KEYSEL_IFID = 1,  /* slot = AS-ingress IFID & 0xff, IFID = Cons ? HF.ingress : HF.egress
+                             (the hf_ingress rule of xdp.c:151-157) */
+};
+
+typedef struct hfv_ctx hfv_ctx;
+
+/* ---- lifetime ----------------------------------------------------------------------
+ * Replaces the mac_key_map creation/pinning part of attachBr (br_loader.cpp:88-151). */
+int hfv_ctx_create(int device, hfv_ctx **out);
+int hfv_ctx_destroy(hfv_ctx *ctx);
+int hfv_ctx_device(const hfv_ctx *ctx);
+void *hfv_ctx_stream(hfv_ctx *ctx);
+int hfv_ctx_set_keysel(hfv_ctx *ctx, int keysel);
+/* Offsets of the current InfoField / HopField inside each record (multiples of 8). */
+int hfv_ctx_set_record_layout(hfv_ctx *ctx, uint32_t inf_off, uint32_t hf_off);
+/* Wait for all work the ctx enqueued on its own stream. */
+int hfv_ctx_synchronize(hfv_ctx *ctx);
+
+/* ---- key table (mac_key_map) -------------------------------------------------------
+ * Updates are made on a host shadow table and published to the GPU at the next batch
+ * boundary (stream-ordered, double-buffered): batches already enqueued keep the table
+ * they were launched with, like RCU readers of the BPF hash map. */
+/* br-loader key add: decodeKey -> aes_key_expansion -> aes_cmac_subkeys -> keep K1
+ * -> map update (br_loader.cpp:182-229). */
+int hfv_key_add(hfv_ctx *ctx, uint32_t index, const struct aes_key *key);
+/* Same, from the 24-character base64 form the CLI takes (decodeKey, br_loader.cpp:65-73). */
+int hfv_key_add_b64(hfv_ctx *ctx, uint32_t index, const char *base64);
+/* Map::update with a ready hop_key (what br-loader writes to the map). */
+int hfv_key_set_hop_key(hfv_ctx *ctx, uint32_t index, const struct hop_key *hk);
+/* br-loader key remove: Map::erase (br_loader.cpp:231-261); the slot then fails closed.
+ * Returns -ENOENT if the slot was empty (the BPF map erase fails the same way). */
+int hfv_key_remove(hfv_ctx *ctx, uint32_t index);
+/* Map lookup: copies the slot's hop_key, -ENOENT if empty. */
+int hfv_key_get(hfv_ctx *ctx, uint32_t index, struct hop_key *out);
+
+/* ---- data path ----------------------------------------------------------------------
+ * Fused per-packet verify over fixed-layout records: build macinput from the record's
+ * InfoField/HopField with the AS-ingress beta rule (path_processing.h:39-81), select the
+ * key (keysel), one-block CMAC (aes.h:129-141), 48-bit compare (xdp.c:89-90).
+ * recs: n records of `stride` bytes (8-byte aligned, stride % 8 == 0). */
+int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                       void *stream);
+/* verify_hop_field (xdp.c:77-91) for n prepared inputs: macinput[i] against the 48-bit
+ * expected[i] (low 48 bits of the LE u64, as defer_verify_hop_field stores it).
+ * key_index: per-packet slot (device u8 array) or NULL for slot 0. */
+int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t *expected,
+                         const uint8_t *key_index, size_t n, uint64_t *pass_bits, void *stream);
+/* Parity mode: full 16-byte AES-CMAC tags of n one-block messages (aes_cmac_16bytes).
+ * A missing key yields an all-zero tag. */
+int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_index, size_t n,
+                  struct aes_cmac *tags, void *stream);
+/* Host-memory batch (config 5 path): records and bitmap in HOST memory; the call stages
+ * them through pinned buffers with H2D / kernel / D2H overlapped over chunks and returns
+ * when pass_bits is complete. */
+int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits);
+
+/* ---- key-schedule kernels ------------------------------------------------------------
+ * AES-128 key expansion + CMAC K1 on the GPU, one key per lane: device raw keys[n] ->
+ * device hop_keys[n] (same bytes as aes_key_expansion + aes_cmac_subkeys). */
+int hfv_expand_keys(hfv_ctx *ctx, const struct aes_key *keys, size_t n, struct hop_key *out, void *stream);
+/* Bulk install: n raw host keys into slots first..first+n-1, expanded on the GPU. */
+int hfv_key_add_batch(hfv_ctx *ctx, uint32_t first, const struct aes_key *keys, size_t n);
+
+/* ---- synthetic traffic ---------------------------------------------------------------
+ * Writes n synthetic 64 B SCION records with valid MACs under the
+ * ctx's CURRENT key table and keysel (1/16 corrupted), records first_index.. of `seed`'s
+ * stream.  stride >= 64, 16-byte aligned. */
+int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t seed, uint64_t first_index,
+                    void *stream);
+
+/* ---- host helpers ---------------------------------------------------------------------- */
+/* Scalar verify_hop_field on the host (SURVEY.md 8b v) for control-plane checks. */
+int hfv_verify_macinput(const struct macinput *mi, uint64_t expected, const struct hop_key *key);
+/* Base64 key decode with the reference's rules (exactly 24 chars, last two dropped). */
+int hfv_decode_key_b64(const char *base64, struct aes_key *key);
+/* Device memory helpers for C hosts without a framework allocator. */
+int hfv_dev_alloc(hfv_ctx *ctx, size_t bytes, void **ptr);
+int hfv_dev_free(hfv_ctx *ctx, void *ptr);
+int hfv_memcpy_h2d(hfv_ctx *ctx, void *dst, const void *src, size_t bytes);
+int hfv_memcpy_d2h(hfv_ctx *ctx, void *dst, const void *src, size_t bytes);
+const char *hfv_last_error(void);
+int hfv_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

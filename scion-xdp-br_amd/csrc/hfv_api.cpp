@@ -1,0 +1,467 @@
+// hfv_api.cpp -- the C ABI of libscionhfv.so (include/scion_hfv.h): per-GPU context,
+// the mac_key_map-equivalent key table, and the batch entry points.
+//
+// Key table publication (replaces map updates under RCU, br_loader.cpp:221-222): key
+// add/remove edit a host shadow; the next data-path call on any stream copies the shadow
+// into the inactive one of two device tables (through a pinned staging image), then
+// launches with it.  A device table is rewritten only after the work that last read it
+// has completed (tracked with one event per table), so in-flight batches keep a stable
+// table.
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime.h>
+
+#include "hfv_internal.h"
+
+namespace hfv {
+
+static thread_local char g_err[256];
+
+int fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static int hip_fail(hipError_t e, const char *what)
+{
+    return fail(-EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                          \
+    do {                                                       \
+        hipError_t e_ = (expr);                                \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr);      \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace hfv
+
+using namespace hfv;
+
+struct hfv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    LaunchGeom geom{};
+    int keysel = HFV_KEYSEL_ZERO;
+    uint32_t inf_off = HFV_REC_INF_OFF, hf_off = HFV_REC_HF_OFF;
+    // host shadow of mac_key_map
+    hop_key shadow[HFV_MAX_KEYS];
+    uint32_t valid[8] = {0};
+    bool dirty = true;
+    // publication
+    DevKeyTable *host_img = nullptr;      // pinned staging image
+    hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
+    DevKeyTable *dev_tab[2] = {nullptr, nullptr};
+    hipEvent_t tab_done[2] = {nullptr, nullptr};   // last reader of dev_tab[i] finished
+    int active = 0;
+    // host-batch staging (hfv_verify_records_host)
+    hipStream_t hstream[2] = {nullptr, nullptr};
+    uint8_t *h_pin[2] = {nullptr, nullptr};
+    uint8_t *d_rec[2] = {nullptr, nullptr};
+    uint64_t *h_bits[2] = {nullptr, nullptr};
+    uint64_t *d_bits[2] = {nullptr, nullptr};
+    size_t host_chunk = 0;
+};
+
+static hipStream_t pick_stream(hfv_ctx *ctx, void *stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+// Make the shadow table visible to work enqueued next on `st`; returns the table to use.
+static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
+{
+    if (ctx->dirty) {
+        int next = ctx->active ^ 1;
+        // wait (host) until the previous copy out of the staging image has been consumed
+        HIP_TRY(hipEventSynchronize(ctx->img_free));
+        for (uint32_t k = 0; k < HFV_MAX_KEYS; ++k) {
+            uint32_t dk[4 * kDevKeyRows];
+            if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) compile_dev_key(&ctx->shadow[k], dk);
+            else memset(dk, 0, sizeof dk);
+            for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->rows[r][k], dk + 4 * r, 16);
+        }
+        memcpy(ctx->host_img->valid, ctx->valid, sizeof ctx->valid);
+        // the device table may only be overwritten after its last reader completed
+        HIP_TRY(hipStreamWaitEvent(st, ctx->tab_done[next], 0));
+        HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevKeyTable), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(ctx->img_free, st));
+        ctx->active = next;
+        ctx->dirty = false;
+    }
+    *out = ctx->dev_tab[ctx->active];
+    return 0;
+}
+
+static int after_launch(hfv_ctx *ctx, hipStream_t st, int err, const char *what)
+{
+    if (err != hipSuccess) return hip_fail((hipError_t)err, what);
+    HIP_TRY(hipEventRecord(ctx->tab_done[ctx->active], st));
+    return 0;
+}
+
+extern "C" {
+
+const char *hfv_last_error(void) { return g_err; }
+int hfv_abi_version(void) { return HFV_ABI_VERSION; }
+
+int hfv_ctx_create(int device, hfv_ctx **out)
+{
+    if (!out) return fail(-EINVAL, "out is NULL");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(-ENODEV, "no HIP device available");
+    if (device < 0 || device >= count) return fail(-ENODEV, "device %d out of range (%d devices)", device, count);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(-ENODEV, "device %d is %s; libscionhfv is built for gfx950 only", device, prop.gcnArchName);
+    DeviceGuard g(device);
+    hfv_ctx *c = new (std::nothrow) hfv_ctx();
+    if (!c) return fail(-ENOMEM, "ctx allocation");
+    c->device = device;
+    int rc = 0;
+    do {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = -EIO; break; }
+        if (hipHostMalloc((void **)&c->host_img, sizeof(DevKeyTable), hipHostMallocDefault) != hipSuccess) { rc = -ENOMEM; break; }
+        if (hipEventCreateWithFlags(&c->img_free, hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
+        for (int i = 0; i < 2; ++i) {
+            if (hipMalloc((void **)&c->dev_tab[i], sizeof(DevKeyTable)) != hipSuccess) { rc = -ENOMEM; break; }
+            if (hipMemset(c->dev_tab[i], 0, sizeof(DevKeyTable)) != hipSuccess) { rc = -EIO; break; }
+            if (hipEventCreateWithFlags(&c->tab_done[i], hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
+        }
+        if (rc) break;
+        if (query_geometry(device, &c->geom) != 0) { rc = -EIO; break; }
+    } while (0);
+    if (rc) {
+        hfv_ctx_destroy(c);
+        return fail(rc, "hfv_ctx_create failed on device %d", device);
+    }
+    memset(c->shadow, 0, sizeof c->shadow);
+    *out = c;
+    return 0;
+}
+
+int hfv_ctx_destroy(hfv_ctx *ctx)
+{
+    if (!ctx) return 0;
+    DeviceGuard g(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->hstream[i]) { (void)hipStreamSynchronize(ctx->hstream[i]); (void)hipStreamDestroy(ctx->hstream[i]); }
+        if (ctx->h_pin[i]) (void)hipHostFree(ctx->h_pin[i]);
+        if (ctx->h_bits[i]) (void)hipHostFree(ctx->h_bits[i]);
+        if (ctx->d_rec[i]) (void)hipFree(ctx->d_rec[i]);
+        if (ctx->d_bits[i]) (void)hipFree(ctx->d_bits[i]);
+        if (ctx->tab_done[i]) { (void)hipEventSynchronize(ctx->tab_done[i]); (void)hipEventDestroy(ctx->tab_done[i]); }
+        if (ctx->dev_tab[i]) (void)hipFree(ctx->dev_tab[i]);
+    }
+    if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
+    if (ctx->host_img) (void)hipHostFree(ctx->host_img);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return 0;
+}
+
+int hfv_ctx_device(const hfv_ctx *ctx) { return ctx ? ctx->device : -1; }
+void *hfv_ctx_stream(hfv_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int hfv_ctx_set_keysel(hfv_ctx *ctx, int keysel)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (keysel != HFV_KEYSEL_ZERO && keysel != HFV_KEYSEL_IFID) return fail(-EINVAL, "unknown keysel %d", keysel);
+    ctx->keysel = keysel;
+    return 0;
+}
+
+int hfv_ctx_set_record_layout(hfv_ctx *ctx, uint32_t inf_off, uint32_t hf_off)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if ((inf_off & 7) || (hf_off & 7)) return fail(-EINVAL, "INF/HF offsets must be multiples of 8");
+    ctx->inf_off = inf_off;
+    ctx->hf_off = hf_off;
+    return 0;
+}
+
+int hfv_ctx_synchronize(hfv_ctx *ctx)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// ---- key table ------------------------------------------------------------------------
+
+int hfv_key_set_hop_key(hfv_ctx *ctx, uint32_t index, const struct hop_key *hk)
+{
+    if (!ctx || !hk) return fail(-EINVAL, "null argument");
+    if (index >= HFV_MAX_KEYS) return fail(-EINVAL, "key index %u >= %d", index, HFV_MAX_KEYS);
+    ctx->shadow[index] = *hk;
+    ctx->valid[index >> 5] |= 1u << (index & 31);
+    ctx->dirty = true;
+    return 0;
+}
+
+int hfv_key_add(hfv_ctx *ctx, uint32_t index, const struct aes_key *key)
+{
+    if (!ctx || !key) return fail(-EINVAL, "null argument");
+    hop_key hk;
+    hop_key_from_key(key->b, &hk);   // aes_key_expansion + aes_cmac_subkeys, K1 kept
+    return hfv_key_set_hop_key(ctx, index, &hk);
+}
+
+int hfv_key_add_b64(hfv_ctx *ctx, uint32_t index, const char *base64)
+{
+    struct aes_key k;
+    int rc = hfv_decode_key_b64(base64, &k);
+    if (rc) return rc;
+    return hfv_key_add(ctx, index, &k);
+}
+
+int hfv_key_remove(hfv_ctx *ctx, uint32_t index)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (index >= HFV_MAX_KEYS) return fail(-EINVAL, "key index %u >= %d", index, HFV_MAX_KEYS);
+    if (!((ctx->valid[index >> 5] >> (index & 31)) & 1u)) return fail(-ENOENT, "key slot %u is empty", index);
+    ctx->valid[index >> 5] &= ~(1u << (index & 31));
+    memset(&ctx->shadow[index], 0, sizeof(hop_key));
+    ctx->dirty = true;
+    return 0;
+}
+
+int hfv_key_get(hfv_ctx *ctx, uint32_t index, struct hop_key *out)
+{
+    if (!ctx || !out) return fail(-EINVAL, "null argument");
+    if (index >= HFV_MAX_KEYS) return fail(-EINVAL, "key index %u >= %d", index, HFV_MAX_KEYS);
+    if (!((ctx->valid[index >> 5] >> (index & 31)) & 1u)) return fail(-ENOENT, "key slot %u is empty", index);
+    *out = ctx->shadow[index];
+    return 0;
+}
+
+int hfv_key_add_batch(hfv_ctx *ctx, uint32_t first, const struct aes_key *keys, size_t n)
+{
+    if (!ctx || (!keys && n)) return fail(-EINVAL, "null argument");
+    if ((size_t)first + n > HFV_MAX_KEYS) return fail(-EINVAL, "slots %u..%zu exceed %d", first, first + n, HFV_MAX_KEYS);
+    if (n == 0) return 0;
+    DeviceGuard g(ctx->device);
+    uint8_t *d_raw = nullptr;
+    hop_key *d_hk = nullptr;
+    HIP_TRY(hipMalloc((void **)&d_raw, 16 * n));
+    if (hipMalloc((void **)&d_hk, sizeof(hop_key) * n) != hipSuccess) {
+        (void)hipFree(d_raw);
+        return fail(-ENOMEM, "hipMalloc");
+    }
+    int rc = 0;
+    if (hipMemcpyAsync(d_raw, keys, 16 * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) rc = -EIO;
+    if (!rc && launch_expand_keys(d_raw, n, d_hk, nullptr, 0, ctx->stream) != 0) rc = -EIO;
+    hop_key *tmp = (hop_key *)malloc(sizeof(hop_key) * n);
+    if (!tmp) rc = -ENOMEM;
+    if (!rc && hipMemcpyAsync(tmp, d_hk, sizeof(hop_key) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = -EIO;
+    if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = -EIO;
+    if (!rc)
+        for (size_t i = 0; i < n; ++i) hfv_key_set_hop_key(ctx, first + (uint32_t)i, &tmp[i]);
+    free(tmp);
+    (void)hipFree(d_raw);
+    (void)hipFree(d_hk);
+    return rc ? fail(rc, "device key expansion failed") : 0;
+}
+
+// ---- data path ------------------------------------------------------------------------
+
+int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits, void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!recs || !pass_bits) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)recs & 7) || (stride & 7) || ((uintptr_t)pass_bits & 7))
+        return fail(-EINVAL, "records, stride and bitmap must be 8-byte aligned");
+    if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
+        return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
+                                  ctx->hf_off, pass_bits, st);
+    return after_launch(ctx, st, e, "verify_records launch");
+}
+
+int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t *expected, const uint8_t *key_index,
+                         size_t n, uint64_t *pass_bits, void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!mi || !expected || !pass_bits) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)mi & 15) || ((uintptr_t)expected & 7) || ((uintptr_t)pass_bits & 7))
+        return fail(-EINVAL, "macinputs must be 16-byte aligned, expected/bitmap 8-byte aligned");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    int e = launch_verify_macinputs(ctx->geom, tab, mi, expected, key_index, n, pass_bits, st);
+    return after_launch(ctx, st, e, "verify_macinputs launch");
+}
+
+int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_index, size_t n, struct aes_cmac *tags,
+                  void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!mi || !tags) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)mi & 15) || ((uintptr_t)tags & 15)) return fail(-EINVAL, "macinputs/tags must be 16-byte aligned");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    int e = launch_cmac_tags(ctx->geom, tab, mi, key_index, n, tags, st);
+    return after_launch(ctx, st, e, "cmac_tags launch");
+}
+
+int hfv_expand_keys(hfv_ctx *ctx, const struct aes_key *keys, size_t n, struct hop_key *out, void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!keys || !out) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)keys & 15) || ((uintptr_t)out & 15)) return fail(-EINVAL, "buffers must be 16-byte aligned");
+    DeviceGuard g(ctx->device);
+    int e = launch_expand_keys((const uint8_t *)keys, n, out, nullptr, 0, pick_stream(ctx, stream));
+    if (e != hipSuccess) return hip_fail((hipError_t)e, "expand_keys launch");
+    return 0;
+}
+
+int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t seed, uint64_t first_index,
+                    void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!recs) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)recs & 15) || (stride & 15) || stride < 64)
+        return fail(-EINVAL, "records must be 16-byte aligned with stride >= 64, multiple of 16");
+    if (ctx->inf_off != HFV_REC_INF_OFF || ctx->hf_off != HFV_REC_HF_OFF)
+        return fail(-EINVAL, "the generator writes the default 64 B layout only");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    int e = launch_gen_records(ctx->geom, tab, ctx->keysel, (uint8_t *)recs, stride, n, seed, first_index, st);
+    return after_launch(ctx, st, e, "gen_records launch");
+}
+
+// Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
+// streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.
+int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!recs || !pass_bits) return fail(-EINVAL, "null buffer");
+    if ((stride & 7) || stride < (size_t)ctx->hf_off + 12 || stride < (size_t)ctx->inf_off + 8)
+        return fail(-EINVAL, "bad stride %zu", stride);
+    DeviceGuard g(ctx->device);
+    const size_t chunk = (size_t)1 << 20;   // records per chunk (64 MiB at 64 B)
+    if (ctx->host_chunk < chunk * stride) {
+        for (int i = 0; i < 2; ++i) {
+            if (ctx->h_pin[i]) (void)hipHostFree(ctx->h_pin[i]);
+            if (ctx->d_rec[i]) (void)hipFree(ctx->d_rec[i]);
+            if (ctx->h_bits[i]) (void)hipHostFree(ctx->h_bits[i]);
+            if (ctx->d_bits[i]) (void)hipFree(ctx->d_bits[i]);
+            ctx->h_pin[i] = ctx->d_rec[i] = nullptr;
+            ctx->h_bits[i] = ctx->d_bits[i] = nullptr;
+            if (!ctx->hstream[i]) HIP_TRY(hipStreamCreateWithFlags(&ctx->hstream[i], hipStreamNonBlocking));
+            HIP_TRY(hipHostMalloc((void **)&ctx->h_pin[i], chunk * stride, hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void **)&ctx->d_rec[i], chunk * stride));
+            HIP_TRY(hipHostMalloc((void **)&ctx->h_bits[i], chunk / 8, hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void **)&ctx->d_bits[i], chunk / 8));
+        }
+        ctx->host_chunk = chunk * stride;
+    }
+    size_t nchunks = (n + chunk - 1) / chunk;
+    size_t pending_words[2] = {0, 0};
+    size_t pending_first[2] = {0, 0};
+    for (size_t c = 0; c < nchunks + 2; ++c) {
+        int slot = (int)(c & 1);
+        hipStream_t st = ctx->hstream[slot];
+        if (c >= 2) {   // retire chunk c-2 (same slot)
+            HIP_TRY(hipStreamSynchronize(st));
+            memcpy(pass_bits + pending_first[slot], ctx->h_bits[slot], pending_words[slot] * 8);
+        }
+        if (c >= nchunks) continue;
+        size_t first = c * chunk, cnt = n - first < chunk ? n - first : chunk;
+        memcpy(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, cnt * stride);
+        HIP_TRY(hipMemcpyAsync(ctx->d_rec[slot], ctx->h_pin[slot], cnt * stride, hipMemcpyHostToDevice, st));
+        DevKeyTable *tab;
+        int rc = publish_keys(ctx, st, &tab);
+        if (rc) return rc;
+        int e = launch_verify_records(ctx->geom, tab, ctx->keysel, ctx->d_rec[slot], stride, cnt, ctx->inf_off,
+                                      ctx->hf_off, ctx->d_bits[slot], st);
+        rc = after_launch(ctx, st, e, "verify_records launch");
+        if (rc) return rc;
+        size_t words = (cnt + 63) / 64;
+        HIP_TRY(hipMemcpyAsync(ctx->h_bits[slot], ctx->d_bits[slot], words * 8, hipMemcpyDeviceToHost, st));
+        pending_words[slot] = words;
+        pending_first[slot] = first / 64;
+    }
+    return 0;
+}
+
+// ---- memory helpers -------------------------------------------------------------------
+
+int hfv_dev_alloc(hfv_ctx *ctx, size_t bytes, void **ptr)
+{
+    if (!ctx || !ptr) return fail(-EINVAL, "null argument");
+    DeviceGuard g(ctx->device);
+    if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess) return fail(-ENOMEM, "hipMalloc(%zu)", bytes);
+    return 0;
+}
+
+int hfv_dev_free(hfv_ctx *ctx, void *ptr)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipFree(ptr));
+    return 0;
+}
+
+int hfv_memcpy_h2d(hfv_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int hfv_memcpy_d2h(hfv_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+}  // extern "C"

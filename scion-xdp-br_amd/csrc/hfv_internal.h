@@ -1,0 +1,50 @@
+// hfv_internal.h -- shared between the host API (hfv_api.cpp, hfv_aes_host.cpp) and the
+// kernel launchers (hfv_kernels.hip).  Not installed.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/scion_hfv.h"
+#include "hfv_tables.h"
+
+namespace hfv {
+
+// error reporting (thread-local message, negative errno return)
+int fail(int code, const char *fmt, ...);
+
+// host AES (hfv_aes_host.cpp)
+void expand_key(const uint8_t key[16], uint32_t w[44]);
+void encrypt_block(const uint32_t rk[44], const uint32_t in[4], uint32_t out[4]);
+void hop_key_from_key(const uint8_t key[16], hop_key *hk);
+void compile_dev_key(const hop_key *hk, uint32_t dk[4 * kDevKeyRows]);
+
+// Device key table as the kernels see it: dev keys in round-major order
+// [kDevKeyRows][HFV_MAX_KEYS] x 16 B, followed by the 256-bit valid bitmap.
+struct DevKeyTable {
+    uint32_t rows[kDevKeyRows][HFV_MAX_KEYS][4];
+    uint32_t valid[8];
+};
+
+enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
+
+struct LaunchGeom {
+    int num_cus;
+    int blocks_per_cu_single;   // KEYSEL_ZERO record verify (64 KiB LDS)
+    int blocks_per_cu_multi;    // per-lane keys (64 KiB + 48 KiB LDS)
+};
+
+// kernel launchers (hfv_kernels.hip); return hipError_t as int
+int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
+                          size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits,
+                          void *stream);
+int launch_verify_macinputs(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint64_t *expected,
+                            const uint8_t *kidx, size_t n, uint64_t *bits, void *stream);
+int launch_cmac_tags(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint8_t *kidx, size_t n,
+                     void *tags, void *stream);
+int launch_expand_keys(const uint8_t *raw, size_t n, hop_key *out, DevKeyTable *tab, uint32_t first_slot,
+                       void *stream);
+int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
+                       size_t n, uint64_t seed, uint64_t first_index, void *stream);
+int query_geometry(int device, LaunchGeom *g);
+
+}  // namespace hfv

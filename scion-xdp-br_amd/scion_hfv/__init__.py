@@ -1,0 +1,271 @@
+"""Python binding of libscionhfv.so (include/scion_hfv.h) -- SCION hop-field AES-CMAC
+verification on MI355X.
+
+Thin ctypes layer over the C ABI; every data-path call goes to the HIP kernels.  There is
+no CPU fallback: if the shared library or a GPU is missing, calls raise HfvError.
+
+Device buffers may be given as torch CUDA tensors (``data_ptr()`` is used) or raw integer
+device pointers.  torch is imported before the library is loaded so that both share one
+HIP runtime in the process (device pointers and streams then interoperate).
+"""
+import ctypes
+import errno
+import os
+import sys
+
+try:  # load torch's HIP runtime first (same soname as /opt/rocm's), see module docstring
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for C-style use
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libscionhfv.so")
+
+KEYSEL_ZERO = 0
+KEYSEL_IFID = 1
+MAX_KEYS = 256
+REC_INF_OFF = 40
+REC_HF_OFF = 48
+REC_SIZE = 64
+BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic HBM bytes per verified record
+
+
+class HfvError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (rc={code} {errno.errorcode.get(-code, '')})")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libscionhfv.so once; raise HfvError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HfvError(-errno.ENOENT, f"{LIB_PATH} not built (run `make -C {PKG_ROOT}`)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32, u64, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sigs = {
+        "hfv_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "hfv_ctx_destroy": (i32, [vp]),
+        "hfv_ctx_device": (i32, [vp]),
+        "hfv_ctx_stream": (vp, [vp]),
+        "hfv_ctx_set_keysel": (i32, [vp, i32]),
+        "hfv_ctx_set_record_layout": (i32, [vp, u32, u32]),
+        "hfv_ctx_synchronize": (i32, [vp]),
+        "hfv_key_add": (i32, [vp, u32, vp]),
+        "hfv_key_add_b64": (i32, [vp, u32, ctypes.c_char_p]),
+        "hfv_key_set_hop_key": (i32, [vp, u32, vp]),
+        "hfv_key_remove": (i32, [vp, u32]),
+        "hfv_key_get": (i32, [vp, u32, vp]),
+        "hfv_key_add_batch": (i32, [vp, u32, vp, sz]),
+        "hfv_verify_records": (i32, [vp, vp, sz, sz, vp, vp]),
+        "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+        "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
+        "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
+        "hfv_expand_keys": (i32, [vp, vp, sz, vp, vp]),
+        "hfv_gen_records": (i32, [vp, vp, sz, sz, u64, u64, vp]),
+        "hfv_verify_macinput": (i32, [vp, u64, vp]),
+        "hfv_decode_key_b64": (i32, [ctypes.c_char_p, vp]),
+        "hfv_dev_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "hfv_dev_free": (i32, [vp, vp]),
+        "hfv_memcpy_h2d": (i32, [vp, vp, vp, sz]),
+        "hfv_memcpy_d2h": (i32, [vp, vp, vp, sz]),
+        "hfv_last_error": (ctypes.c_char_p, []),
+        "hfv_abi_version": (i32, []),
+        "aes_key_expansion": (None, [vp, vp]),
+        "aes_cypher": (i32, [vp, vp, vp]),
+        "aes_cmac_subkeys": (None, [vp, vp]),
+        "aes_cmac": (None, [vp, sz, vp, vp, vp]),
+        "aes_cmac_no_loops": (None, [vp, sz, vp, vp, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise HfvError(rc, lib().hfv_last_error().decode(errors="replace"))
+    return rc
+
+
+def _ptr(x):
+    """Device/host pointer from a torch tensor, numpy array, ctypes buffer or int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return ctypes.cast(x, ctypes.c_void_p).value
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+# ---- aes.h surface (host, control plane) ---------------------------------------------------
+
+def aes_key_expansion(key: bytes) -> bytes:
+    out = ctypes.create_string_buffer(176)
+    lib().aes_key_expansion(bytes(key), out)
+    return out.raw
+
+
+def aes_cypher(block: bytes, sched: bytes) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().aes_cypher(bytes(block), bytes(sched), out)
+    return out.raw
+
+
+def aes_cmac_subkeys(sched: bytes):
+    out = ctypes.create_string_buffer(32)
+    lib().aes_cmac_subkeys(bytes(sched), out)
+    return out.raw[:16], out.raw[16:]
+
+
+def aes_cmac(data: bytes, key: bytes, no_loops=False) -> bytes:
+    sched = aes_key_expansion(key)
+    k1, k2 = aes_cmac_subkeys(sched)
+    out = ctypes.create_string_buffer(16)
+    fn = lib().aes_cmac_no_loops if no_loops else lib().aes_cmac
+    fn(bytes(data), len(data), sched, k1 + k2, out)
+    return out.raw
+
+
+def hop_key(key: bytes) -> bytes:
+    """192-byte struct hop_key image (br/src/bpf/common.h:87-91) for a raw 16-byte key."""
+    sched = aes_key_expansion(key)
+    k1, _ = aes_cmac_subkeys(sched)
+    return sched + k1
+
+
+def decode_key_b64(s: str) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    _check(lib().hfv_decode_key_b64(s.encode(), out))
+    return out.raw
+
+
+def verify_macinput(macinput: bytes, expected: int, hop_key_bytes) -> bool:
+    return bool(lib().hfv_verify_macinput(bytes(macinput), expected, None if hop_key_bytes is None else bytes(hop_key_bytes)))
+
+
+# ---- context --------------------------------------------------------------------------------
+
+class Ctx:
+    """One per GPU (hfv_ctx).  Mirrors the br-loader key commands and the XDP verify step."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        _check(lib().hfv_ctx_create(device, ctypes.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().hfv_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib().hfv_ctx_stream(self._h)
+
+    def set_keysel(self, keysel):
+        _check(lib().hfv_ctx_set_keysel(self._h, keysel))
+
+    def set_record_layout(self, inf_off, hf_off):
+        _check(lib().hfv_ctx_set_record_layout(self._h, inf_off, hf_off))
+
+    def synchronize(self):
+        _check(lib().hfv_ctx_synchronize(self._h))
+
+    # key table (br-loader key add / remove)
+    def key_add(self, index, key: bytes):
+        _check(lib().hfv_key_add(self._h, index, bytes(key)))
+
+    def key_add_b64(self, index, b64: str):
+        _check(lib().hfv_key_add_b64(self._h, index, b64.encode()))
+
+    def key_set_hop_key(self, index, hk: bytes):
+        _check(lib().hfv_key_set_hop_key(self._h, index, bytes(hk)))
+
+    def key_remove(self, index):
+        _check(lib().hfv_key_remove(self._h, index))
+
+    def key_get(self, index) -> bytes:
+        out = ctypes.create_string_buffer(192)
+        _check(lib().hfv_key_get(self._h, index, out))
+        return out.raw
+
+    def key_add_batch(self, first, keys: bytes):
+        assert len(keys) % 16 == 0
+        _check(lib().hfv_key_add_batch(self._h, first, bytes(keys), len(keys) // 16))
+
+    # data path (device buffers)
+    def verify_records(self, recs, n, pass_bits, stride=REC_SIZE, stream=None):
+        _check(lib().hfv_verify_records(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _stream(stream)))
+
+    def verify_macinputs(self, mi, expected, n, pass_bits, key_index=None, stream=None):
+        _check(lib().hfv_verify_macinputs(self._h, _ptr(mi), _ptr(expected), _ptr(key_index), n, _ptr(pass_bits),
+                                          _stream(stream)))
+
+    def cmac_tags(self, mi, n, tags, key_index=None, stream=None):
+        _check(lib().hfv_cmac_tags(self._h, _ptr(mi), _ptr(key_index), n, _ptr(tags), _stream(stream)))
+
+    def expand_keys(self, keys, n, out, stream=None):
+        _check(lib().hfv_expand_keys(self._h, _ptr(keys), n, _ptr(out), _stream(stream)))
+
+    def gen_records(self, recs, n, seed, first_index=0, stride=REC_SIZE, stream=None):
+        _check(lib().hfv_gen_records(self._h, _ptr(recs), stride, n, seed, first_index, _stream(stream)))
+
+    # host buffers (pinned staging, H2D/kernel/D2H overlapped)
+    def verify_records_host(self, recs, n, pass_bits, stride=REC_SIZE):
+        _check(lib().hfv_verify_records_host(self._h, _ptr(recs), stride, n, _ptr(pass_bits)))
+
+
+# ---- batch sharding across GPUs ------------------------------------------------
+
+def shard_range(n, world, rank):
+    """Contiguous slice of n packets for `rank`, cut on 64-packet boundaries so each rank's
+    verdict bitmap is a whole-word slice of the global bitmap."""
+    words = (n + 63) // 64
+    w0 = words * rank // world
+    w1 = words * (rank + 1) // world
+    return min(64 * w0, n), min(64 * w1, n)
+
+
+def bits_to_bool(words, n):
+    """Expand a uint64 verdict bitmap (numpy) to a bool array of n entries."""
+    import numpy as np
+    b = np.unpackbits(np.ascontiguousarray(words).view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]
+if sys.version_info < (3, 8):  # pragma: no cover
+    raise RuntimeError("python >= 3.8 required")

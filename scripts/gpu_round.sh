@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprof kernel-trace summary.
+# Each GPU step has its own time limit; a crash/abort/timeout (status >= 2 other than a
+# plain pytest failure) stops the script so nothing else touches the GPU afterwards.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {   # step <name> <timeout-s> <cmd...>
+    local name=$1 t=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -n 25 "$OUT/$name.log"
+    return $rc
+}
+MODE=${1:-all}
+if [[ $MODE == all || $MODE == test ]]; then
+    step pytest_gpu 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+    rc=$?; [[ $rc -gt 1 ]] && exit $rc
+fi
+if [[ $MODE == all || $MODE == bench ]]; then
+    step bench 600 python bench.py || exit $?
+fi
+if [[ $MODE == all || $MODE == prof ]]; then
+    step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+        python3 bench.py --steps 50 --warmup 5 --big-n 0 --cpu-budget 0 --no-host-e2e || exit $?
+    find $OUT/prof -name "*stats*.csv" | head
+fi

@@ -1,0 +1,115 @@
+"""The C-ABI library loads and exports what include/*.h declares; the host-side
+control-plane API (aes.h surface, base64 key decode, scalar verify_hop_field) matches the
+reference's known answers.  CPU only: no compute call here touches a GPU."""
+import ctypes
+import errno
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import orc
+import scion_hfv as hfv
+
+ROOT = orc.ROOT
+KAT = json.load(open(os.path.join(orc.GOLDEN, "kat.json")))
+
+
+def declared_functions():
+    names = set()
+    for h in ("scion_hfv.h", "hfv_aes.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(\w+)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_lib_exports_every_declared_symbol():
+    names = declared_functions()
+    assert {"hfv_verify_records", "hfv_key_add", "aes_cmac", "aes_key_expansion"} <= names
+    out = subprocess.run(["nm", "-D", "--defined-only", hfv.LIB_PATH], check=True, capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = sorted(names - exported)
+    assert not missing, missing
+    assert "AES_SBox" in exported
+    L = hfv.lib()
+    assert L.hfv_abi_version() == 1
+
+
+def test_exported_sbox():
+    sbox = bytes((ctypes.c_uint8 * 256).in_dll(hfv.lib(), "AES_SBox"))
+    L = orc.oracle()
+    L.orc_sbox.restype = ctypes.POINTER(ctypes.c_uint8 * 256)
+    assert sbox == bytes(L.orc_sbox().contents)
+
+
+def test_host_aes_api_kats():
+    key = bytes.fromhex(KAT["key"])
+    sched = hfv.aes_key_expansion(key)
+    assert [f"{w:08x}" for w in np.frombuffer(sched, dtype="<u4")] == KAT["expansion_le_words"]
+    k1, k2 = hfv.aes_cmac_subkeys(sched)
+    assert (k1.hex(), k2.hex()) == (KAT["k1"], KAT["k2"])
+    for v in KAT["blocks"]:
+        assert hfv.aes_cypher(bytes.fromhex(v["in"]), hfv.aes_key_expansion(bytes.fromhex(v["key"]))).hex() == v["out"]
+    msg = bytes.fromhex(KAT["cmac_msg"])
+    for v in KAT["cmac"]:
+        assert hfv.aes_cmac(msg[: v["len"]], key).hex() == v["tag"]
+        assert hfv.aes_cmac(msg[: v["len"]], key, no_loops=True).hex() == v["tag"]
+    long_msg = bytes(range(200))
+    for v in KAT["no_loops_quirk"]:
+        assert hfv.aes_cmac(long_msg[: v["len"]], key, no_loops=True).hex() == v["tag"]
+        assert hfv.aes_cmac(long_msg[: v["len"]], key).hex() == v["tag_full"]
+
+
+def test_host_aes_api_random_vs_oracle():
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        assert hfv.hop_key(key) == orc.hop_key(key)
+        for L in (0, 1, 15, 16, 17, 33, 64, 65, 100):
+            data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            assert hfv.aes_cmac(data, key) == orc.cmac(data, key)
+            assert hfv.aes_cmac(data, key, no_loops=True) == orc.cmac(data, key, no_loops=True)
+
+
+def test_decode_key_b64_br_convention():
+    br = KAT["br_key"]
+    assert hfv.decode_key_b64(br["base64"]).hex() == br["key"]
+    assert hfv.decode_key_b64("MjIyMjIyMjIyMjIyMjIyMg==") == b"2222222222222222"
+    with pytest.raises(hfv.HfvError) as e:
+        hfv.decode_key_b64("MTEx")  # br_loader.cpp:70: "Key has invalid length"
+    assert e.value.code == -errno.EINVAL
+    with pytest.raises(hfv.HfvError):
+        hfv.decode_key_b64("MTExMTExMTExMTExMTExM!==")
+
+
+def test_scalar_verify_macinput():
+    g = orc.load_golden("hf_single.npz")
+    hk = g["hop_keys"][0].tobytes()
+    truth = np.unpackbits(g["pass_bits"].view(np.uint8), bitorder="little")
+    for i in range(200):
+        expected = int.from_bytes(g["records"][i, 54:60].tobytes(), "little")
+        assert hfv.verify_macinput(g["macinputs"][i].tobytes(), expected, hk) == bool(truth[i])
+    assert not hfv.verify_macinput(g["macinputs"][0].tobytes(), 0, None)  # no key: fail closed
+
+
+def test_ctx_without_gpu_reports_enodev():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(hfv.HfvError) as e:
+        hfv.Ctx(0)
+    assert e.value.code == -errno.ENODEV
+
+
+def test_shard_ranges_cover_word_aligned():
+    for n in (0, 1, 63, 64, 1000, 1 << 20, (1 << 20) + 5):
+        for world in (1, 2, 3, 4, 8):
+            cuts = [hfv.shard_range(n, world, r) for r in range(world)]
+            assert cuts[0][0] == 0 and cuts[-1][1] == n
+            for (a0, a1), (b0, b1) in zip(cuts, cuts[1:]):
+                assert a1 == b0 and a0 % 64 == 0

@@ -1,0 +1,155 @@
+"""The CPU checker is pinned before it is trusted (CPU only).
+
+* against the reference's own known-answer vectors (aes/src/test/aes_test.cpp:33-245,
+  transcribed into tests/golden/kat.json);
+* against the reference aes.c compiled from /root/reference (oracle/_ref), when present;
+* against the committed hop-field fixtures whose bitmaps/tags the reference produced.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import orc
+
+KAT = json.load(open(os.path.join(orc.GOLDEN, "kat.json")))
+
+
+def test_sbox_generated_matches_fips197():
+    L = orc.oracle()
+    L.orc_sbox.restype = ctypes.POINTER(ctypes.c_uint8 * 256)
+    s = bytes(L.orc_sbox().contents)
+    assert s[0x00] == 0x63 and s[0x01] == 0x7C and s[0x53] == 0xED and s[0xFF] == 0x16
+    assert len(set(s)) == 256  # a permutation
+
+
+def test_key_expansion_kat():
+    sched = ctypes.create_string_buffer(176)
+    orc.oracle().orc_key_expansion(bytes.fromhex(KAT["key"]), sched)
+    words = list(np.frombuffer(sched.raw, dtype="<u4"))
+    assert [f"{w:08x}" for w in words] == KAT["expansion_le_words"]
+
+
+def test_block_kats():
+    L = orc.oracle()
+    for v in KAT["blocks"]:
+        sched = ctypes.create_string_buffer(176)
+        L.orc_key_expansion(bytes.fromhex(v["key"]), sched)
+        out = ctypes.create_string_buffer(16)
+        L.orc_cypher(bytes.fromhex(v["in"]), sched, out)
+        assert out.raw.hex() == v["out"]
+
+
+def test_subkeys_kat():
+    L = orc.oracle()
+    sched = ctypes.create_string_buffer(176)
+    L.orc_key_expansion(bytes.fromhex(KAT["key"]), sched)
+    k1, k2 = ctypes.create_string_buffer(16), ctypes.create_string_buffer(16)
+    L.orc_cmac_subkeys(sched, k1, k2)
+    assert k1.raw.hex() == KAT["k1"] and k2.raw.hex() == KAT["k2"]
+
+
+@pytest.mark.parametrize("no_loops", [False, True])
+def test_cmac_rfc4493(no_loops):
+    msg = bytes.fromhex(KAT["cmac_msg"])
+    key = bytes.fromhex(KAT["key"])
+    for v in KAT["cmac"]:
+        assert orc.cmac(msg[: v["len"]], key, no_loops).hex() == v["tag"]
+
+
+def test_testpy_blocks_and_br_key():
+    key = bytes.fromhex(KAT["key"])
+    for v in KAT["testpy_blocks"]:
+        assert orc.cmac(bytes.fromhex(v["data"]), key).hex() == v["tag"]
+    br = KAT["br_key"]
+    assert orc.hop_key(bytes.fromhex(br["key"])).hex() == br["hop_key"]
+    assert orc.cmac(bytes.fromhex(br["macinput"]), bytes.fromhex(br["key"])).hex() == br["tag"]
+    assert orc.cmac(bytes(16), bytes.fromhex(br["key"])).hex() == br["zero_tag"]
+
+
+def test_no_loops_quirk_over_64_bytes():
+    key = bytes.fromhex(KAT["key"])
+    long_msg = bytes(range(200))
+    for v in KAT["no_loops_quirk"]:
+        assert orc.cmac(long_msg[: v["len"]], key, no_loops=True).hex() == v["tag"]
+        assert orc.cmac(long_msg[: v["len"]], key).hex() == v["tag_full"]
+
+
+@pytest.mark.parametrize("name,keysel", [("hf_single.npz", 0), ("hf_ifid256.npz", 1)])
+def test_hf_fixtures(name, keysel):
+    g = orc.load_golden(name)
+    recs = g["records"]
+    # the generator restatement reproduces the committed records byte for byte
+    again = orc.gen_records(len(recs), g["hop_keys"].reshape(-1), keysel)
+    assert np.array_equal(again, recs)
+    bits = orc.verify_records(recs, g["hop_keys"].reshape(-1), g["valid"], keysel)
+    assert np.array_equal(bits, g["pass_bits"])
+    mi, exp, kidx = orc.macinputs_from_records(recs)
+    assert np.array_equal(mi, g["macinputs"])
+    if keysel == 1:
+        assert np.array_equal(kidx, g["key_index"])
+    # generator truth: exactly the uncorrupted records verify
+    truth = orc.expected_pass_rule(len(recs))
+    got = np.unpackbits(g["pass_bits"].view(np.uint8), bitorder="little")[: len(recs)].astype(bool)
+    assert np.array_equal(truth, got)
+
+
+def test_oracle_matches_reference_build_random():
+    R = orc.reference()
+    if R is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(7)
+    raw = orc.gen_key_table(256)
+    hk, valid = orc.key_table(raw)
+    # random bytes in every field, including garbage headers and flags
+    recs = rng.integers(0, 256, size=(5000, 64), dtype=np.uint8)
+    for keysel in (0, 1):
+        ours = orc.verify_records(recs, hk, valid, keysel)
+        for aesni in (0, 1):
+            ref = orc.ref_verify_records(recs, raw, hk, valid, keysel, aesni=aesni)
+            assert np.array_equal(ours, ref)
+    # random CMAC lengths vs the reference's aes_cmac
+    key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    for L in list(range(0, 70)) + [127, 128, 129, 255]:
+        data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        sched = ctypes.create_string_buffer(176)
+        R.aes_key_expansion(key, sched)
+        sk = ctypes.create_string_buffer(32)
+        R.aes_cmac_subkeys(sched, sk)
+        for fn, nl in (("aes_cmac", False), ("aes_cmac_no_loops", True)):
+            mac = ctypes.create_string_buffer(16)
+            getattr(R, fn)(data, ctypes.c_size_t(L), sched, sk, mac)
+            assert orc.cmac(data, key, no_loops=nl) == mac.raw, (fn, L)
+
+
+def test_missing_key_fails_closed_and_partial_table():
+    g = orc.load_golden("hf_ifid256.npz")
+    recs, hk = g["records"], g["hop_keys"].reshape(-1)
+    valid = g["valid"].copy()
+    valid[0] = 0  # drop slots 0..31
+    bits = orc.verify_records(recs, hk, valid, 1)
+    got = np.unpackbits(bits.view(np.uint8), bitorder="little")[: len(recs)].astype(bool)
+    kidx = g["key_index"]
+    assert not got[kidx < 32].any()
+    base = np.unpackbits(g["pass_bits"].view(np.uint8), bitorder="little")[: len(recs)].astype(bool)
+    assert np.array_equal(got[kidx >= 32], base[kidx >= 32])
+    none = orc.verify_records(recs, hk, np.zeros(8, np.uint32), 0)
+    assert not none.any()
+
+
+def test_ragged_and_empty():
+    g = orc.load_golden("hf_single.npz")
+    recs, hk, valid = g["records"], g["hop_keys"].reshape(-1), g["valid"]
+    full = orc.verify_records(recs, hk, valid, 0)
+    for n in (0, 1, 63, 64, 65, 999):
+        b = orc.verify_records(recs[:n], hk, valid, 0, n=n)
+        assert len(b) == (n + 63) // 64
+        if n:
+            exp = full[: len(b)].copy()
+            if n % 64:
+                exp[-1] &= np.uint64((1 << (n % 64)) - 1)
+            assert np.array_equal(b, exp)
+    # threaded split agrees with the single-threaded pass
+    assert np.array_equal(orc.verify_records(recs, hk, valid, 0, nthreads=5), full)

@@ -16,8 +16,8 @@
  *     human-readable message for the calling thread.  No C++ exception crosses the ABI.
  *   - Batch buffers (records, macinputs, tags, pass bitmaps) are DEVICE pointers (hipMalloc,
  *     hipMallocManaged or a framework allocation on the ctx's GPU) unless a function says
- *     otherwise.  `stream` is a hipStream_t passed as void*; NULL selects the ctx's own
- *     stream.  Calls enqueue work and return; completion is stream-ordered.
+ *     otherwise.  `stream` is a hipStream_t passed as void*; NULL is HIP's default
+ *     stream (hfv_ctx_stream() returns a private non-blocking stream of the ctx).  Calls enqueue work and return; completion is stream-ordered.
  *   - Verdict output: bit (i % 64) of pass_bits[i / 64] is 1 iff packet i's hop field
  *     verifies; bits for i >= n in the last word are 0.  A missing key fails closed
  *     (xdp.c:83-84).
@@ -96,6 +96,23 @@ int hfv_key_set_hop_key(hfv_ctx *ctx, uint32_t index, const struct hop_key *hk);
 int hfv_key_remove(hfv_ctx *ctx, uint32_t index);
 /* Map lookup: copies the slot's hop_key, -ENOENT if empty. */
 int hfv_key_get(hfv_ctx *ctx, uint32_t index, struct hop_key *out);
+
+/* ---- pinned key map ------------------------------------------------------------------
+ * A file-backed mac_key_map that other processes update while the data plane runs, the
+ * analogue of the bpffs-pinned map /sys/fs/bpf/<br>/mac_key_map (br_loader.cpp:119-126,
+ * 191, 221-222).  Path: $HFV_PIN_DIR/<br>/mac_key_map, HFV_PIN_DIR defaults to /dev/shm/hfv.
+ * Writers serialise with flock; readers see whole updates (seqlock). */
+int hfv_keymap_path(const char *br, char *out, size_t len);
+/* Map::update of one slot, creating the map file if needed. */
+int hfv_keymap_update(const char *path, uint32_t index, const struct hop_key *hk);
+/* Map::erase of one slot; -ENOENT if it was empty. */
+int hfv_keymap_erase(const char *path, uint32_t index);
+/* Consistent snapshot of all HFV_MAX_KEYS slots and the 256-bit valid mask. */
+int hfv_keymap_read(const char *path, struct hop_key *slots, uint32_t *valid);
+/* reusePinnedMap: the ctx reloads its key table from the pinned map whenever the map
+ * changed, at the next batch boundary; hfv_key_add/remove on the ctx then write through
+ * to the map.  The map is created empty if it does not exist. */
+int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path);
 
 /* ---- data path ----------------------------------------------------------------------
  * Fused per-packet verify over fixed-layout records: build macinput from the record's

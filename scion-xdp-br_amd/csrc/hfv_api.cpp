@@ -74,7 +74,10 @@ struct hfv_ctx {
     DevKeyTable *host_img = nullptr;      // pinned staging image
     hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
     DevKeyTable *dev_tab[2] = {nullptr, nullptr};
-    hipEvent_t tab_done[2] = {nullptr, nullptr};   // last reader of dev_tab[i] finished
+    hipEvent_t tab_done[2] = {nullptr, nullptr};   // scratch events for the reader fence
+    hipStream_t readers[2][8] = {};                // streams that launched with dev_tab[i]
+    int nreaders[2] = {0, 0};
+    bool readers_overflow[2] = {false, false};
     int active = 0;
     // host-batch staging (hfv_verify_records_host)
     hipStream_t hstream[2] = {nullptr, nullptr};
@@ -83,13 +86,30 @@ struct hfv_ctx {
     uint64_t *h_bits[2] = {nullptr, nullptr};
     uint64_t *d_bits[2] = {nullptr, nullptr};
     size_t host_chunk = 0;
+    // attached pinned key map
+    const void *keymap = nullptr;
+    uint32_t keymap_seq = 0xffffffffu;
+    char keymap_path[4096] = {0};
 };
 
-static hipStream_t pick_stream(hfv_ctx *ctx, void *stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+// NULL is HIP's default stream, as for any HIP API taking a stream.
+static hipStream_t pick_stream(hfv_ctx *, void *stream) { return (hipStream_t)stream; }
+
+// Streams that launched with each device table since it was last published.  Before a
+// table is rewritten, the publishing stream waits for an event recorded on each of them, so
+// no per-launch event is needed on the hot path.
+static void note_reader(hfv_ctx *ctx, hipStream_t st);
 
 // Make the shadow table visible to work enqueued next on `st`; returns the table to use.
 static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
 {
+    if (ctx->keymap) {   // pick up updates other processes made to the pinned map
+        uint32_t seq = keymap_seq(ctx->keymap);
+        if (seq != ctx->keymap_seq) {
+            ctx->keymap_seq = keymap_snapshot(ctx->keymap, ctx->shadow, ctx->valid);
+            ctx->dirty = true;
+        }
+    }
     if (ctx->dirty) {
         int next = ctx->active ^ 1;
         // wait (host) until the previous copy out of the staging image has been consumed
@@ -101,8 +121,19 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
             for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->rows[r][k], dk + 4 * r, 16);
         }
         memcpy(ctx->host_img->valid, ctx->valid, sizeof ctx->valid);
-        // the device table may only be overwritten after its last reader completed
-        HIP_TRY(hipStreamWaitEvent(st, ctx->tab_done[next], 0));
+        // the device table may only be overwritten after every launch that read it completed
+        if (ctx->readers_overflow[next]) {
+            HIP_TRY(hipDeviceSynchronize());
+        } else {
+            for (int r = 0; r < ctx->nreaders[next]; ++r) {
+                hipStream_t rs = ctx->readers[next][r];
+                if (rs == st) continue;   // same stream: ordered already
+                HIP_TRY(hipEventRecord(ctx->tab_done[next], rs));
+                HIP_TRY(hipStreamWaitEvent(st, ctx->tab_done[next], 0));
+            }
+        }
+        ctx->nreaders[next] = 0;
+        ctx->readers_overflow[next] = false;
         HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevKeyTable), hipMemcpyHostToDevice, st));
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
@@ -112,10 +143,19 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
     return 0;
 }
 
+static void note_reader(hfv_ctx *ctx, hipStream_t st)
+{
+    int a = ctx->active;
+    for (int r = 0; r < ctx->nreaders[a]; ++r)
+        if (ctx->readers[a][r] == st) return;
+    if (ctx->nreaders[a] < 8) ctx->readers[a][ctx->nreaders[a]++] = st;
+    else ctx->readers_overflow[a] = true;
+}
+
 static int after_launch(hfv_ctx *ctx, hipStream_t st, int err, const char *what)
 {
     if (err != hipSuccess) return hip_fail((hipError_t)err, what);
-    HIP_TRY(hipEventRecord(ctx->tab_done[ctx->active], st));
+    note_reader(ctx, st);
     return 0;
 }
 
@@ -176,6 +216,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->tab_done[i]) { (void)hipEventSynchronize(ctx->tab_done[i]); (void)hipEventDestroy(ctx->tab_done[i]); }
         if (ctx->dev_tab[i]) (void)hipFree(ctx->dev_tab[i]);
     }
+    keymap_close(ctx->keymap);
     if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
     if (ctx->host_img) (void)hipHostFree(ctx->host_img);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -217,6 +258,10 @@ int hfv_key_set_hop_key(hfv_ctx *ctx, uint32_t index, const struct hop_key *hk)
 {
     if (!ctx || !hk) return fail(-EINVAL, "null argument");
     if (index >= HFV_MAX_KEYS) return fail(-EINVAL, "key index %u >= %d", index, HFV_MAX_KEYS);
+    if (ctx->keymap) {
+        int rc = hfv_keymap_update(ctx->keymap_path, index, hk);
+        if (rc) return rc;
+    }
     ctx->shadow[index] = *hk;
     ctx->valid[index >> 5] |= 1u << (index & 31);
     ctx->dirty = true;
@@ -244,8 +289,32 @@ int hfv_key_remove(hfv_ctx *ctx, uint32_t index)
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     if (index >= HFV_MAX_KEYS) return fail(-EINVAL, "key index %u >= %d", index, HFV_MAX_KEYS);
     if (!((ctx->valid[index >> 5] >> (index & 31)) & 1u)) return fail(-ENOENT, "key slot %u is empty", index);
+    if (ctx->keymap) {
+        int rc = hfv_keymap_erase(ctx->keymap_path, index);
+        if (rc) return rc;
+    }
     ctx->valid[index >> 5] &= ~(1u << (index & 31));
     memset(&ctx->shadow[index], 0, sizeof(hop_key));
+    ctx->dirty = true;
+    return 0;
+}
+
+int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
+{
+    if (!ctx || !path) return fail(-EINVAL, "null argument");
+    if (strlen(path) >= sizeof ctx->keymap_path) return fail(-ENAMETOOLONG, "path too long");
+    const void *m = nullptr;
+    int rc = keymap_open_ro(path, &m);
+    if (rc == -ENOENT) {   // create an empty pinned map, as attachBr creates mac_key_map
+        rc = hfv_keymap_update(path, 0, &ctx->shadow[0]);
+        if (!rc) rc = hfv_keymap_erase(path, 0);
+        if (!rc) rc = keymap_open_ro(path, &m);
+    }
+    if (rc) return fail(rc, "cannot attach key map %s", path);
+    keymap_close(ctx->keymap);
+    ctx->keymap = m;
+    strcpy(ctx->keymap_path, path);
+    ctx->keymap_seq = keymap_snapshot(m, ctx->shadow, ctx->valid);
     ctx->dirty = true;
     return 0;
 }

@@ -47,4 +47,10 @@ int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, 
                        size_t n, uint64_t seed, uint64_t first_index, void *stream);
 int query_geometry(int device, LaunchGeom *g);
 
+// pinned key map (hfv_keymap.cpp)
+int keymap_open_ro(const char *path, const void **mapping);
+void keymap_close(const void *mapping);
+uint32_t keymap_seq(const void *mapping);
+uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8]);
+
 }  // namespace hfv

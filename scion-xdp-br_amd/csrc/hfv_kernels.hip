@@ -17,6 +17,7 @@
 //   * Persistent grid (a few blocks per CU) so the 64 KiB table fill is paid once per
 //     block; the next tile's record bytes are prefetched while the current tile computes.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "hfv_internal.h"
 
@@ -529,19 +530,24 @@ int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, 
     return (int)hipGetLastError();
 }
 
+// Persistent-grid size: blocks per CU for the record-verify kernels.  One 16-wave block per
+// CU pays the 64 KiB table fill once per CU; HFV_BLOCKS_PER_CU overrides it (capped by the
+// occupancy query, which on ROCm 7.2 can over-report for SGPR-heavy kernels).
 int query_geometry(int device, LaunchGeom *g)
 {
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
+    int want = 1;
+    if (const char *env = getenv("HFV_BLOCKS_PER_CU")) want = atoi(env) > 0 ? atoi(env) : 1;
     int b = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_verify_records<HFV_KEYSEL_ZERO, kBlockRec>, kBlockRec, 0);
     if (e != hipSuccess) return (int)e;
-    g->blocks_per_cu_single = b > 0 ? b : 1;
+    g->blocks_per_cu_single = b > 0 ? (want < b ? want : b) : 1;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_verify_records<HFV_KEYSEL_IFID, kBlockRec>, kBlockRec, 0);
     if (e != hipSuccess) return (int)e;
-    g->blocks_per_cu_multi = b > 0 ? b : 1;
+    g->blocks_per_cu_multi = b > 0 ? (want < b ? want : b) : 1;
     return 0;
 }
 

@@ -111,11 +111,15 @@ def _ptr(x):
 
 
 def _stream(stream):
+    """hipStream_t for a call: an explicit int/torch stream, else torch's current stream
+    (so work stays ordered with torch ops on the same buffers), else HIP's default stream."""
     if stream is None:
+        if torch is not None and torch.cuda.is_initialized():
+            return torch.cuda.current_stream().cuda_stream or None
         return None
     if isinstance(stream, int):
-        return stream
-    return stream.cuda_stream  # torch.cuda.Stream
+        return stream or None
+    return stream.cuda_stream or None  # torch.cuda.Stream
 
 
 # ---- aes.h surface (host, control plane) ---------------------------------------------------

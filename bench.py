@@ -82,14 +82,9 @@ def make_ctx(device, keysel):
 
 
 def kernel_ms(ctx, recs, n, bits, stream, reps):
-    """Mean duration of one verify launch, HIP events recorded on the launch stream."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in evs:
-        a.record(stream)
-        ctx.verify_records(recs, n, bits, stream=stream)
-        b.record(stream)
-    stream.synchronize()
-    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    """Mean/median execution time of one verify launch on `stream`, from the dispatch's own
+    start/stop timestamps (hipExtLaunchKernel events, hfv_verify_records_timed)."""
+    ts = sorted(ctx.verify_records_timed(recs, n, bits, stream=stream) for _ in range(reps))
     return float(np.mean(ts)), float(ts[len(ts) // 2])
 
 
@@ -159,7 +154,7 @@ def main():
     n = args.n
 
     ctx = make_ctx(local, keysel)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.current_stream().cuda_stream   # int handle (0 = default stream)
     recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
     ctx.gen_records(recs, n, SEED_RECORDS, first_index=rank * n, stream=stream)
     bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
@@ -219,7 +214,7 @@ def main():
                    "parallelism": f"batch-sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_verify_records", "kernel_ms_mean": round(k_mean, 5),
+                     "kernel": "k_verify_records", "variant": ctx.describe(), "kernel_ms_mean": round(k_mean, 5),
                      "kernel_ms_median": round(k_med, 5),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch),
                      "note": f"2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"},

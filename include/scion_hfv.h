@@ -130,6 +130,11 @@ int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t
  * A missing key yields an all-zero tag. */
 int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_index, size_t n,
                   struct aes_cmac *tags, void *stream);
+/* Same as hfv_verify_records, then waits for it and stores the kernel's own execution
+ * time (start/stop timestamps of the dispatch, hipExtLaunchKernel events) in *kernel_ms.
+ * Used by the benchmark to price the kernel against its roofline. */
+int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                             void *stream, float *kernel_ms);
 /* Host-memory batch (config 5 path): records and bitmap in HOST memory; the call stages
  * them through pinned buffers with H2D / kernel / D2H overlapped over chunks and returns
  * when pass_bits is complete. */
@@ -159,6 +164,8 @@ int hfv_dev_alloc(hfv_ctx *ctx, size_t bytes, void **ptr);
 int hfv_dev_free(hfv_ctx *ctx, void *ptr);
 int hfv_memcpy_h2d(hfv_ctx *ctx, void *dst, const void *src, size_t bytes);
 int hfv_memcpy_d2h(hfv_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* Writes a one-line description of the kernel variants the ctx launches. */
+int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len);
 const char *hfv_last_error(void);
 int hfv_abi_version(void);
 

@@ -90,6 +90,8 @@ struct hfv_ctx {
     const void *keymap = nullptr;
     uint32_t keymap_seq = 0xffffffffu;
     char keymap_path[4096] = {0};
+    // dispatch timing (hfv_verify_records_timed)
+    hipEvent_t tev[2] = {nullptr, nullptr};
 };
 
 // NULL is HIP's default stream, as for any HIP API taking a stream.
@@ -217,6 +219,8 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->dev_tab[i]) (void)hipFree(ctx->dev_tab[i]);
     }
     keymap_close(ctx->keymap);
+    for (int i = 0; i < 2; ++i)
+        if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
     if (ctx->host_img) (void)hipHostFree(ctx->host_img);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -375,6 +379,44 @@ int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
     int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
                                   ctx->hf_off, pass_bits, st);
     return after_launch(ctx, st, e, "verify_records launch");
+}
+
+int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                             void *stream, float *kernel_ms)
+{
+    if (!ctx || !kernel_ms) return fail(-EINVAL, "null argument");
+    *kernel_ms = 0.0f;
+    if (n == 0) return 0;
+    if (!recs || !pass_bits) return fail(-EINVAL, "null buffer");
+    if (((uintptr_t)recs & 7) || (stride & 7) || ((uintptr_t)pass_bits & 7))
+        return fail(-EINVAL, "records, stride and bitmap must be 8-byte aligned");
+    if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
+        return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
+    DeviceGuard g(ctx->device);
+    for (int i = 0; i < 2; ++i)
+        if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
+                                  ctx->hf_off, pass_bits, st, ctx->tev[0], ctx->tev[1]);
+    rc = after_launch(ctx, st, e, "verify_records launch");
+    if (rc) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->tev[1]));
+    HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
+int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
+{
+    if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");
+    const KernelVariant &a = ctx->geom.single, &b = ctx->geom.multi;
+    snprintf(buf, len,
+             "zero: block=%d pf=%d tab=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d grid=%dx%d",
+             a.block, a.pf, a.tab, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab, ctx->geom.num_cus,
+             b.blocks_per_cu);
+    return 0;
 }
 
 int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t *expected, const uint8_t *key_index,

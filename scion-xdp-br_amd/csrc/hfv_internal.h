@@ -27,16 +27,23 @@ struct DevKeyTable {
 
 enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 
+struct KernelVariant {
+    int block;           // threads per block
+    int pf;              // record tiles loaded ahead of the one computed (1 or 2)
+    int tab;             // round tables in LDS: 2 (T0/T1, 64 KiB) or 4 (T0..T3, 128 KiB)
+    int blocks_per_cu;   // persistent grid = num_cus * blocks_per_cu
+};
+
 struct LaunchGeom {
     int num_cus;
-    int blocks_per_cu_single;   // KEYSEL_ZERO record verify (64 KiB LDS)
-    int blocks_per_cu_multi;    // per-lane keys (64 KiB + 48 KiB LDS)
+    KernelVariant single;   // KEYSEL_ZERO record verify
+    KernelVariant multi;    // KEYSEL_IFID record verify (per-lane keys in LDS)
 };
 
 // kernel launchers (hfv_kernels.hip); return hipError_t as int
 int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits,
-                          void *stream);
+                          void *stream, void *ev_start = nullptr, void *ev_stop = nullptr);
 int launch_verify_macinputs(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint64_t *expected,
                             const uint8_t *kidx, size_t n, uint64_t *bits, void *stream);
 int launch_cmac_tags(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint8_t *kidx, size_t n,

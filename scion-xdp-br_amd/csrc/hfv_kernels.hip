@@ -17,7 +17,11 @@
 //   * Persistent grid (a few blocks per CU) so the 64 KiB table fill is paid once per
 //     block; the next tile's record bytes are prefetched while the current tile computes.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_ext.h>
 
 #include "hfv_internal.h"
 
@@ -34,27 +38,42 @@ __constant__ uint32_t c_t0[256] = {T0V64(0), T0V64(64), T0V64(128), T0V64(192)};
 #undef T0V8
 #undef T0V
 
-constexpr int kTabDwords = 256 * 64;            // 64 KiB
-__shared__ uint32_t s_ttab[kTabDwords];
+// Round tables in LDS.  Layout (byte address of table t at index x for lane L):
+//   (x << 8) | ((t & 1) << 7) | ((L & 31) << 2) | ((t >> 1) << 16)
+// TAB = 2 keeps T0/T1 (64 KiB) and derives T2/T3 by a 16-bit rotation; TAB = 4 stores all
+// four (128 KiB) and needs no rotation.
+__shared__ uint32_t s_tab64[16384];
+__shared__ uint32_t s_tab128[32768];
 __shared__ uint4 s_keys[kDevKeyRows * HFV_MAX_KEYS];   // 48 KiB, round-major
 __shared__ uint32_t s_valid[8];
 
-// v_perm selectors: address byte 1 <- state byte k, byte 0 <- base byte 0
-constexpr uint32_t SEL_B0 = 0x0c0c0400u, SEL_B1 = 0x0c0c0500u, SEL_B2 = 0x0c0c0600u, SEL_B3 = 0x0c0c0700u;
+// v_perm selector for state byte k: address byte 0 <- base byte 0 (copy + T0/T1 bit),
+// byte 1 <- state byte k, byte 2 <- base byte 2 (T2/T3 bit), byte 3 <- 0.
+constexpr uint32_t sel_byte(int k) { return 0x0c020400u | (uint32_t(k) << 8); }
+constexpr uint32_t SEL_B0 = sel_byte(0), SEL_B1 = sel_byte(1), SEL_B2 = sel_byte(2), SEL_B3 = sel_byte(3);
 
 __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 
+template <int TAB>
 __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, uint32_t sel)
 {
     uint32_t a = __builtin_amdgcn_perm(w, base, sel);
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_ttab) + a);
+    if constexpr (TAB == 4)
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab128) + a);
+    else
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab64) + a);
 }
 
+template <int TAB>
 __device__ __forceinline__ void fill_ttab()
 {
-    for (int e = threadIdx.x; e < kTabDwords; e += blockDim.x) {
-        uint32_t t = c_t0[e >> 6];
-        s_ttab[e] = (e & 32) ? ((t << 8) | (t >> 24)) : t;
+    constexpr int kDwords = TAB == 4 ? 32768 : 16384;
+    uint32_t *dst = TAB == 4 ? s_tab128 : s_tab64;
+#pragma unroll 4
+    for (int e = threadIdx.x; e < kDwords; e += blockDim.x) {
+        uint32_t t = c_t0[(e >> 6) & 255];
+        int rot = 8 * (((e >> 5) & 1) | ((e >> 13) & 2));   // table index * 8
+        dst[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
     }
 }
 
@@ -69,20 +88,27 @@ __device__ __forceinline__ void fill_keys(const DevKeyTable *tab)
 // AES rounds on a column-word state (s[c] = LE u32 of column c)
 // ---------------------------------------------------------------------------------------
 struct Lane {
-    uint32_t b0, b1;   // LDS byte offsets of this lane's T0 / T1 copies
+    uint32_t b0, b1, b2, b3;   // LDS byte offsets of this lane's copies of T0..T3
 };
 
+template <int TAB>
 __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const Lane &l)
 {
     const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
     uint32_t n[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu(s[c], l.b0, SEL_B0);
-        uint32_t b = tlu(s[(c + 1) & 3], l.b1, SEL_B1);
-        uint32_t x = tlu(s[(c + 2) & 3], l.b0, SEL_B2);
-        uint32_t d = tlu(s[(c + 3) & 3], l.b1, SEL_B3);
-        n[c] = a ^ b ^ r[c] ^ rot16(x ^ d);
+        uint32_t a = tlu<TAB>(s[c], l.b0, SEL_B0);
+        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b1, SEL_B1);
+        if constexpr (TAB == 4) {
+            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, SEL_B2);
+            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, SEL_B3);
+            n[c] = a ^ b ^ x ^ d ^ r[c];
+        } else {
+            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, SEL_B2);
+            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, SEL_B3);
+            n[c] = a ^ b ^ r[c] ^ rot16(x ^ d);
+        }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) s[c] = n[c];
@@ -90,38 +116,49 @@ __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const
 
 // Round 1 for a whitened macinput whose bytes 0,1,8,14,15 are key-only: the five lookups
 // they feed are folded into rk1' (device key row 11, see hfv_tables.h).
+template <int TAB>
 __device__ __forceinline__ void round1_macinput(uint32_t s[4], const uint4 &rk1p, const Lane &l)
 {
-    uint32_t n0 = tlu(s[1], l.b1, SEL_B1) ^ rot16(tlu(s[2], l.b0, SEL_B2)) ^ rk1p.x;
-    uint32_t n1 = tlu(s[1], l.b0, SEL_B0) ^ tlu(s[2], l.b1, SEL_B1) ^ rot16(tlu(s[0], l.b1, SEL_B3)) ^ rk1p.y;
-    uint32_t n2 = tlu(s[3], l.b1, SEL_B1) ^ rot16(tlu(s[0], l.b0, SEL_B2) ^ tlu(s[1], l.b1, SEL_B3)) ^ rk1p.z;
-    uint32_t n3 = tlu(s[3], l.b0, SEL_B0) ^ rot16(tlu(s[1], l.b0, SEL_B2) ^ tlu(s[2], l.b1, SEL_B3)) ^ rk1p.w;
+    uint32_t n0, n1, n2, n3;
+    if constexpr (TAB == 4) {
+        n0 = tlu<TAB>(s[1], l.b1, SEL_B1) ^ tlu<TAB>(s[2], l.b2, SEL_B2) ^ rk1p.x;
+        n1 = tlu<TAB>(s[1], l.b0, SEL_B0) ^ tlu<TAB>(s[2], l.b1, SEL_B1) ^ tlu<TAB>(s[0], l.b3, SEL_B3) ^ rk1p.y;
+        n2 = tlu<TAB>(s[3], l.b1, SEL_B1) ^ tlu<TAB>(s[0], l.b2, SEL_B2) ^ tlu<TAB>(s[1], l.b3, SEL_B3) ^ rk1p.z;
+        n3 = tlu<TAB>(s[3], l.b0, SEL_B0) ^ tlu<TAB>(s[1], l.b2, SEL_B2) ^ tlu<TAB>(s[2], l.b3, SEL_B3) ^ rk1p.w;
+    } else {
+        n0 = tlu<TAB>(s[1], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[2], l.b0, SEL_B2)) ^ rk1p.x;
+        n1 = tlu<TAB>(s[1], l.b0, SEL_B0) ^ tlu<TAB>(s[2], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[0], l.b1, SEL_B3)) ^ rk1p.y;
+        n2 = tlu<TAB>(s[3], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[0], l.b0, SEL_B2) ^ tlu<TAB>(s[1], l.b1, SEL_B3)) ^ rk1p.z;
+        n3 = tlu<TAB>(s[3], l.b0, SEL_B0) ^ rot16(tlu<TAB>(s[1], l.b0, SEL_B2) ^ tlu<TAB>(s[2], l.b1, SEL_B3)) ^ rk1p.w;
+    }
     s[0] = n0; s[1] = n1; s[2] = n2; s[3] = n3;
 }
 
 // Final round, S(x) taken from byte 1 of T0[x].  All four output columns:
+template <int TAB>
 __device__ __forceinline__ void round_last_full(uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t out[4])
 {
     const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu(s[c], l.b0, SEL_B0);
-        uint32_t b = tlu(s[(c + 1) & 3], l.b0, SEL_B1);
-        uint32_t x = tlu(s[(c + 2) & 3], l.b0, SEL_B2);
-        uint32_t d = tlu(s[(c + 3) & 3], l.b0, SEL_B3);
+        uint32_t a = tlu<TAB>(s[c], l.b0, SEL_B0);
+        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, SEL_B1);
+        uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, SEL_B2);
+        uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, SEL_B3);
         out[c] = __builtin_amdgcn_perm(b, a, 0x0c0c0501u) ^ __builtin_amdgcn_perm(d, x, 0x05010c0cu) ^ r[c];
     }
 }
 
 // Final round, only the 48 bits the verifier compares (tag bytes 0..5, xdp.c:89):
 // column 0 whole, column 1 bytes 0-1 (upper half of the result is don't-care).
+template <int TAB>
 __device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t &t0,
                                               uint32_t &t1)
 {
-    uint32_t a = tlu(s[0], l.b0, SEL_B0), b = tlu(s[1], l.b0, SEL_B1);
-    uint32_t x = tlu(s[2], l.b0, SEL_B2), d = tlu(s[3], l.b0, SEL_B3);
+    uint32_t a = tlu<TAB>(s[0], l.b0, SEL_B0), b = tlu<TAB>(s[1], l.b0, SEL_B1);
+    uint32_t x = tlu<TAB>(s[2], l.b0, SEL_B2), d = tlu<TAB>(s[3], l.b0, SEL_B3);
     t0 = __builtin_amdgcn_perm(b, a, 0x0c0c0501u) ^ __builtin_amdgcn_perm(d, x, 0x05010c0cu) ^ rk.x;
-    uint32_t a1 = tlu(s[1], l.b0, SEL_B0), b1 = tlu(s[2], l.b0, SEL_B1);
+    uint32_t a1 = tlu<TAB>(s[1], l.b0, SEL_B0), b1 = tlu<TAB>(s[2], l.b0, SEL_B1);
     t1 = __builtin_amdgcn_perm(b1, a1, 0x0c0c0501u) ^ rk.y;
 }
 
@@ -151,25 +188,25 @@ struct LdsKey {              // per-lane slot from the LDS copy of the table
 };
 
 // Tag words 0..1 for a record-derived macinput w[] (bytes 0,1,8,14,15 zero).
-template <class K>
+template <int TAB, class K>
 __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &key, const Lane &l, uint32_t &t0,
                                                 uint32_t &t1)
 {
     uint4 k0 = key.row(0);
     uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
-    round1_macinput(s, key.row(11), l);
+    round1_macinput<TAB>(s, key.row(11), l);
 #pragma unroll
-    for (int r = 2; r < 10; ++r) round_full(s, key.row(r), l);
-    round_last_48(s, key.row(10), l, t0, t1);
+    for (int r = 2; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
+    round_last_48<TAB>(s, key.row(10), l, t0, t1);
 }
 
-template <class K>
+template <int TAB, class K>
 __device__ __forceinline__ void cmac_general(const uint32_t w[4], const K &key, const Lane &l, uint32_t s[4])
 {
     uint4 k0 = key.row(0);
     s[0] = w[0] ^ k0.x; s[1] = w[1] ^ k0.y; s[2] = w[2] ^ k0.z; s[3] = w[3] ^ k0.w;
 #pragma unroll
-    for (int r = 1; r < 10; ++r) round_full(s, key.row(r), l);
+    for (int r = 1; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
 }
 
 __device__ __forceinline__ Lane lane_bases()
@@ -178,6 +215,8 @@ __device__ __forceinline__ Lane lane_bases()
     Lane l;
     l.b0 = (lane & 31) << 2;
     l.b1 = l.b0 | 0x80u;
+    l.b2 = l.b0 | 0x10000u;
+    l.b3 = l.b1 | 0x10000u;
     return l;
 }
 
@@ -233,55 +272,72 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
     return t0 == e0 && ((t1 ^ e1) & 0xffffu) == 0;
 }
 
-template <int KEYSEL, int BLOCK>
+// One tile = 64 consecutive records = one wave.  PF tiles are loaded ahead of the one being
+// computed, so the loads of tile t + PF*nwaves overlap the AES rounds of tile t.
+template <int KEYSEL, int TAB>
+__device__ __forceinline__ void verify_tile(const RecWords &cur, uint64_t t, uint64_t n, uint32_t lane, const Lane &l,
+                                            const UniformKey *ukey, uint64_t *__restrict__ bits)
+{
+    uint32_t w[4], t0, t1;
+    rec_macinput(cur, w);
+    bool ok = t * 64 + lane < n;
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+        cmac48_macinput<TAB>(w, *ukey, l, t0, t1);
+    } else {
+        const LdsKey key(rec_key_slot(cur));
+        cmac48_macinput<TAB>(w, key, l, t0, t1);
+        ok = ok && key.ok();
+    }
+    bool pass = ok && rec_tag_matches(cur, t0, t1);
+    uint64_t ballot = __ballot(pass);
+    if (lane == 0) bits[t] = ballot;
+}
+
+template <int KEYSEL, int BLOCK, int PF, int TAB>
 __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
                                                           uint64_t n, uint32_t inf_off, uint32_t hf_off,
                                                           uint64_t *__restrict__ bits)
 {
+    static_assert(PF == 1 || PF == 2, "prefetch depth");
+    static_assert(KEYSEL == HFV_KEYSEL_ZERO || TAB == 2, "per-lane keys need the 64 KiB table layout");
     constexpr uint32_t kWaves = BLOCK / 64;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
     const uint32_t nwaves = gridDim.x * kWaves;
 
-    fill_ttab();
+    fill_ttab<TAB>();
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
 
+    const UniformKey *ukp = nullptr;
+    UniformKey ukey(tab);
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        const UniformKey key(tab);
-        if (!key.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
+        if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
             for (uint64_t t = wave; t < ntiles; t += nwaves)
                 if (lane == 0) bits[t] = 0;
             return;
         }
-        uint64_t t = wave;
-        RecWords cur = load_rec(recs, stride, t * 64 + lane, n - 1, inf_off, hf_off);
+        ukp = &ukey;
+    }
+    const uint64_t last = n - 1;
+    uint64_t t = wave;
+    RecWords cur = load_rec(recs, stride, t * 64 + lane, last, inf_off, hf_off);
+    if constexpr (PF == 1) {
         for (; t < ntiles; t += nwaves) {
-            RecWords nxt = load_rec(recs, stride, (t + nwaves) * 64 + lane, n - 1, inf_off, hf_off);
-            uint32_t w[4], t0, t1;
-            rec_macinput(cur, w);
-            cmac48_macinput(w, key, l, t0, t1);
-            bool pass = rec_tag_matches(cur, t0, t1) && (t * 64 + lane < n);
-            uint64_t ballot = __ballot(pass);
-            if (lane == 0) bits[t] = ballot;
-            cur = nxt;
+            RecWords nx1 = load_rec(recs, stride, (t + nwaves) * 64 + lane, last, inf_off, hf_off);
+            verify_tile<KEYSEL, TAB>(cur, t, n, lane, l, ukp, bits);
+            cur = nx1;
         }
     } else {
-        uint64_t t = wave;
-        RecWords cur = load_rec(recs, stride, t * 64 + lane, n - 1, inf_off, hf_off);
+        RecWords nx1 = load_rec(recs, stride, (t + nwaves) * 64 + lane, last, inf_off, hf_off);
         for (; t < ntiles; t += nwaves) {
-            RecWords nxt = load_rec(recs, stride, (t + nwaves) * 64 + lane, n - 1, inf_off, hf_off);
-            const LdsKey key(rec_key_slot(cur));
-            uint32_t w[4], t0, t1;
-            rec_macinput(cur, w);
-            cmac48_macinput(w, key, l, t0, t1);
-            bool pass = rec_tag_matches(cur, t0, t1) && key.ok() && (t * 64 + lane < n);
-            uint64_t ballot = __ballot(pass);
-            if (lane == 0) bits[t] = ballot;
-            cur = nxt;
+            RecWords nx2 = load_rec(recs, stride, (t + 2 * nwaves) * 64 + lane, last, inf_off, hf_off);
+            verify_tile<KEYSEL, TAB>(cur, t, n, lane, l, ukp, bits);
+            cur = nx1;
+            nx1 = nx2;
         }
     }
 }
@@ -300,7 +356,7 @@ __global__ __launch_bounds__(BLOCK) void k_macinputs(const DevKeyTable *__restri
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
     const uint32_t nwaves = gridDim.x * kWaves;
-    fill_ttab();
+    fill_ttab<2>();
     fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
@@ -311,15 +367,15 @@ __global__ __launch_bounds__(BLOCK) void k_macinputs(const DevKeyTable *__restri
         uint32_t slot = (in && kidx) ? kidx[i] : 0u;
         const LdsKey key(slot);
         uint32_t w[4] = {m.x, m.y, m.z, m.w}, s[4];
-        cmac_general(w, key, l, s);
+        cmac_general<2>(w, key, l, s);
         if constexpr (MODE == kModeTags) {
             uint32_t o[4];
-            round_last_full(s, key.row(10), l, o);
+            round_last_full<2>(s, key.row(10), l, o);
             if (!key.ok()) o[0] = o[1] = o[2] = o[3] = 0;
             if (in) tags[i] = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
             uint32_t t0, t1;
-            round_last_48(s, key.row(10), l, t0, t1);
+            round_last_48<2>(s, key.row(10), l, t0, t1);
             uint2 e = in ? expected[i] : make_uint2(0, 0);
             // actual = tag bytes 0..5 as LE u64 (upper 16 bits zero) == expected (xdp.c:89-90)
             bool pass = in && key.ok() && t0 == e.x && (t1 & 0xffffu) == e.y;
@@ -427,7 +483,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_records(const DevKeyTable *__rest
                                                        uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
                                                        uint64_t seed, uint64_t first_index)
 {
-    fill_ttab();
+    fill_ttab<2>();
     fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
@@ -446,8 +502,8 @@ __global__ __launch_bounds__(BLOCK) void k_gen_records(const DevKeyTable *__rest
         uint32_t slot = keysel == HFV_KEYSEL_IFID ? ((cons ? ing : eg) & 0xffu) : 0u;
         const LdsKey key(slot);
         uint32_t w[4] = {bswap16(beta) << 16, ts_w, hf0, hf1}, s[4], tg4[4];
-        cmac_general(w, key, l, s);
-        round_last_full(s, key.row(10), l, tg4);
+        cmac_general<2>(w, key, l, s);
+        round_last_full<2>(s, key.row(10), l, tg4);
         uint32_t seg = cons ? beta : (beta ^ bswap16(tg4[0] & 0xffffu));
         uint64_t mac = (uint64_t)tg4[0] | ((uint64_t)(tg4[1] & 0xffffu) << 32);
         if ((r2 & 15u) == 0) mac ^= 1ull << ((r2 >> 4) % 48u);
@@ -463,7 +519,6 @@ __global__ __launch_bounds__(BLOCK) void k_gen_records(const DevKeyTable *__rest
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
-constexpr int kBlockRec = 1024;
 constexpr int kBlockAux = 512;
 
 static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
@@ -475,26 +530,39 @@ static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
     return (unsigned)(blocks ? blocks : 1);
 }
 
-int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
-                          size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream)
+using VerifyKernel = void (*)(const DevKeyTable *, const uint8_t *, uint64_t, uint64_t, uint32_t, uint32_t, uint64_t *);
+
+// Record-verify variants (tuning knobs; the default is chosen by scripts/sweep.py data).
+template <int KEYSEL>
+static VerifyKernel pick_verify(const KernelVariant &v)
 {
-    hipStream_t st = (hipStream_t)stream;
-    if (keysel == HFV_KEYSEL_IFID) {
-        unsigned grid = grid_for(n, kBlockRec, g.num_cus, g.blocks_per_cu_multi);
-        hipLaunchKernelGGL((k_verify_records<HFV_KEYSEL_IFID, kBlockRec>), dim3(grid), dim3(kBlockRec), 0, st, tab,
-                           recs, (uint64_t)stride, (uint64_t)n, inf_off, hf_off, bits);
-    } else {
-        unsigned grid = grid_for(n, kBlockRec, g.num_cus, g.blocks_per_cu_single);
-        hipLaunchKernelGGL((k_verify_records<HFV_KEYSEL_ZERO, kBlockRec>), dim3(grid), dim3(kBlockRec), 0, st, tab,
-                           recs, (uint64_t)stride, (uint64_t)n, inf_off, hf_off, bits);
+#define HFV_V(B, P, T) \
+    if (v.block == B && v.pf == P && v.tab == T) return k_verify_records<KEYSEL, B, P, T>;
+    HFV_V(1024, 1, 2) HFV_V(1024, 2, 2) HFV_V(768, 1, 2) HFV_V(768, 2, 2) HFV_V(512, 1, 2) HFV_V(512, 2, 2)
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+        HFV_V(1024, 1, 4) HFV_V(1024, 2, 4) HFV_V(768, 1, 4) HFV_V(768, 2, 4) HFV_V(512, 1, 4) HFV_V(512, 2, 4)
     }
+#undef HFV_V
+    return nullptr;
+}
+
+int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
+                          size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream,
+                          void *ev_start, void *ev_stop)
+{
+    const KernelVariant &v = keysel == HFV_KEYSEL_IFID ? g.multi : g.single;
+    VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(v) : pick_verify<HFV_KEYSEL_ZERO>(v);
+    if (!k) return (int)hipErrorInvalidConfiguration;
+    unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(v.block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0u, tab, recs, (uint64_t)stride, (uint64_t)n, inf_off, hf_off, bits);
     return (int)hipGetLastError();
 }
 
 int launch_verify_macinputs(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint64_t *expected,
                             const uint8_t *kidx, size_t n, uint64_t *bits, void *stream)
 {
-    unsigned grid = grid_for(n, kBlockAux, g.num_cus, 2 * g.blocks_per_cu_multi);
+    unsigned grid = grid_for(n, kBlockAux, g.num_cus, 2);
     hipLaunchKernelGGL((k_macinputs<kModeMacinputs, kBlockAux>), dim3(grid), dim3(kBlockAux), 0, (hipStream_t)stream,
                        tab, (const uint4 *)mi, (const uint2 *)expected, kidx, (uint64_t)n, bits, (uint4 *)nullptr);
     return (int)hipGetLastError();
@@ -503,7 +571,7 @@ int launch_verify_macinputs(const LaunchGeom &g, const DevKeyTable *tab, const v
 int launch_cmac_tags(const LaunchGeom &g, const DevKeyTable *tab, const void *mi, const uint8_t *kidx, size_t n,
                      void *tags, void *stream)
 {
-    unsigned grid = grid_for(n, kBlockAux, g.num_cus, 2 * g.blocks_per_cu_multi);
+    unsigned grid = grid_for(n, kBlockAux, g.num_cus, 2);
     hipLaunchKernelGGL((k_macinputs<kModeTags, kBlockAux>), dim3(grid), dim3(kBlockAux), 0, (hipStream_t)stream, tab,
                        (const uint4 *)mi, (const uint2 *)nullptr, kidx, (uint64_t)n, (uint64_t *)nullptr,
                        (uint4 *)tags);
@@ -530,25 +598,56 @@ int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, 
     return (int)hipGetLastError();
 }
 
-// Persistent-grid size: blocks per CU for the record-verify kernels.  One 16-wave block per
-// CU pays the 64 KiB table fill once per CU; HFV_BLOCKS_PER_CU overrides it (capped by the
-// occupancy query, which on ROCm 7.2 can over-report for SGPR-heavy kernels).
+// Persistent-grid geometry.  Defaults: see DESIGN.md section 4 (measured with
+// scripts/sweep.py).  HFV_KVARIANT="block=768,pf=2,tab=2,bpc=2" overrides the KEYSEL_ZERO
+// kernel and HFV_KVARIANT_IFID the per-lane-key kernel; blocks per CU are capped by the LDS
+// a block needs and by the occupancy query.
+static void parse_variant(const char *env, KernelVariant *v)
+{
+    if (!env) return;
+    const char *p = env;
+    while (*p) {
+        int val = 0;
+        if (sscanf(p, "block=%d", &val) == 1) v->block = val;
+        else if (sscanf(p, "pf=%d", &val) == 1) v->pf = val;
+        else if (sscanf(p, "tab=%d", &val) == 1) v->tab = val;
+        else if (sscanf(p, "bpc=%d", &val) == 1) v->blocks_per_cu = val;
+        const char *c = strchr(p, ',');
+        if (!c) break;
+        p = c + 1;
+    }
+}
+
+static int finish_variant(int keysel, KernelVariant *v)
+{
+    VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(*v) : pick_verify<HFV_KEYSEL_ZERO>(*v);
+    if (!k) return (int)hipErrorInvalidConfiguration;
+    int lds = (v->tab == 4 ? 131072 : 65536) + (keysel == HFV_KEYSEL_IFID ? (int)sizeof(uint4) * kDevKeyRows * HFV_MAX_KEYS + 32 : 0);
+    int by_lds = (160 * 1024) / lds;
+    int by_waves = 32 / (v->block / 64);
+    int occ = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, v->block, 0);
+    if (e != hipSuccess) return (int)e;
+    int cap = by_lds < by_waves ? by_lds : by_waves;
+    if (occ > 0 && occ < cap) cap = occ;
+    if (cap < 1) cap = 1;
+    if (v->blocks_per_cu <= 0 || v->blocks_per_cu > cap) v->blocks_per_cu = cap;
+    return 0;
+}
+
 int query_geometry(int device, LaunchGeom *g)
 {
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    int want = 1;
-    if (const char *env = getenv("HFV_BLOCKS_PER_CU")) want = atoi(env) > 0 ? atoi(env) : 1;
-    int b = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_verify_records<HFV_KEYSEL_ZERO, kBlockRec>, kBlockRec, 0);
-    if (e != hipSuccess) return (int)e;
-    g->blocks_per_cu_single = b > 0 ? (want < b ? want : b) : 1;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_verify_records<HFV_KEYSEL_IFID, kBlockRec>, kBlockRec, 0);
-    if (e != hipSuccess) return (int)e;
-    g->blocks_per_cu_multi = b > 0 ? (want < b ? want : b) : 1;
-    return 0;
+    g->single = KernelVariant{768, 2, 2, 0};
+    g->multi = KernelVariant{1024, 2, 2, 0};
+    parse_variant(getenv("HFV_KVARIANT"), &g->single);
+    parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
+    int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);
+    if (rc) return rc;
+    return finish_variant(HFV_KEYSEL_IFID, &g->multi);
 }
 
 }  // namespace hfv

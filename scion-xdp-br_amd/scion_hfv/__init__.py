@@ -64,6 +64,13 @@ def lib():
         "hfv_key_get": (i32, [vp, u32, vp]),
         "hfv_key_add_batch": (i32, [vp, u32, vp, sz]),
         "hfv_verify_records": (i32, [vp, vp, sz, sz, vp, vp]),
+        "hfv_verify_records_timed": (i32, [vp, vp, sz, sz, vp, vp, ctypes.POINTER(ctypes.c_float)]),
+        "hfv_ctx_describe": (i32, [vp, ctypes.c_char_p, sz]),
+        "hfv_ctx_attach_keymap": (i32, [vp, ctypes.c_char_p]),
+        "hfv_keymap_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
+        "hfv_keymap_update": (i32, [ctypes.c_char_p, u32, vp]),
+        "hfv_keymap_erase": (i32, [ctypes.c_char_p, u32]),
+        "hfv_keymap_read": (i32, [ctypes.c_char_p, vp, vp]),
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
@@ -118,8 +125,8 @@ def _stream(stream):
             return torch.cuda.current_stream().cuda_stream or None
         return None
     if isinstance(stream, int):
-        return stream or None
-    return stream.cuda_stream or None  # torch.cuda.Stream
+        return stream          # 0 is the NULL (default) stream
+    return stream.cuda_stream  # torch.cuda.Stream
 
 
 # ---- aes.h surface (host, control plane) ---------------------------------------------------
@@ -234,6 +241,21 @@ class Ctx:
     def verify_records(self, recs, n, pass_bits, stride=REC_SIZE, stream=None):
         _check(lib().hfv_verify_records(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _stream(stream)))
 
+    def verify_records_timed(self, recs, n, pass_bits, stride=REC_SIZE, stream=None):
+        """Launch, wait, and return the kernel's own execution time in ms (dispatch events)."""
+        ms = ctypes.c_float()
+        _check(lib().hfv_verify_records_timed(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _stream(stream),
+                                              ctypes.byref(ms)))
+        return ms.value
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().hfv_ctx_describe(self._h, buf, 256))
+        return buf.value.decode()
+
+    def attach_keymap(self, path):
+        _check(lib().hfv_ctx_attach_keymap(self._h, path.encode()))
+
     def verify_macinputs(self, mi, expected, n, pass_bits, key_index=None, stream=None):
         _check(lib().hfv_verify_macinputs(self._h, _ptr(mi), _ptr(expected), _ptr(key_index), n, _ptr(pass_bits),
                                           _stream(stream)))
@@ -250,6 +272,30 @@ class Ctx:
     # host buffers (pinned staging, H2D/kernel/D2H overlapped)
     def verify_records_host(self, recs, n, pass_bits, stride=REC_SIZE):
         _check(lib().hfv_verify_records_host(self._h, _ptr(recs), stride, n, _ptr(pass_bits)))
+
+
+# ---- pinned key map (bpffs mac_key_map analogue) --------------------------------------------
+
+def keymap_path(br: str) -> str:
+    buf = ctypes.create_string_buffer(4096)
+    _check(lib().hfv_keymap_path(br.encode(), buf, 4096))
+    return buf.value.decode()
+
+
+def keymap_update(path: str, index: int, hop_key_bytes: bytes):
+    _check(lib().hfv_keymap_update(path.encode(), index, bytes(hop_key_bytes)))
+
+
+def keymap_erase(path: str, index: int):
+    _check(lib().hfv_keymap_erase(path.encode(), index))
+
+
+def keymap_read(path: str):
+    """(dict slot -> 192-byte hop_key, for the occupied slots)"""
+    slots = ctypes.create_string_buffer(192 * MAX_KEYS)
+    valid = (ctypes.c_uint32 * 8)()
+    _check(lib().hfv_keymap_read(path.encode(), slots, valid))
+    return {k: slots.raw[192 * k:192 * k + 192] for k in range(MAX_KEYS) if (valid[k >> 5] >> (k & 31)) & 1}
 
 
 # ---- batch sharding across GPUs (SURVEY.md 8e) ------------------------------------------------

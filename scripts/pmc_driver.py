@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Workload for rocprofv3 --pmc passes: verify 2^20 and 2^24 records (config 2, and config 3
+with --keysel ifid), `reps` launches each, after one untimed generation pass."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scion-xdp-br_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import scion_hfv as hfv  # noqa: E402
+from bench import KEY_1111, SEED_RECORDS, key_table_256  # noqa: E402
+
+
+def main():
+    keysel = sys.argv[1] if len(sys.argv) > 1 else "zero"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
+    torch.cuda.set_device(0)
+    ctx = hfv.Ctx(0)
+    if keysel == "ifid":
+        ctx.key_add_batch(0, key_table_256())
+        ctx.set_keysel(hfv.KEYSEL_IFID)
+    else:
+        ctx.key_add(0, KEY_1111)
+    for n in sizes:
+        recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
+        bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+        ctx.gen_records(recs, n, SEED_RECORDS)
+        for _ in range(reps):
+            ctx.verify_records(recs, n, bits)
+        torch.cuda.synchronize()
+        del recs, bits
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

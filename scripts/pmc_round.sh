@@ -1,0 +1,25 @@
+#!/bin/bash
+# PMC passes over scripts/pmc_driver.py, one rocprofv3 run per counter group (never
+# combined with tracing domains).  Output: gpurun_out/pmc/<group>/...counter_collection.csv
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+KS=${1:-zero}
+OUT=gpurun_out/pmc_$KS
+mkdir -p $OUT
+groups=(
+  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+  "SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"
+  "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+  "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum"
+)
+i=0
+for g in "${groups[@]}"; do
+  i=$((i+1))
+  echo "=== pass $i: $g"
+  timeout -k 10 300 rocprofv3 --pmc $g --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
+      python3 scripts/pmc_driver.py $KS 10 > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 scripts/pmc_summary.py $OUT

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes over scripts/pmc_driver.py: verify launches are grouped
+by batch (a k_gen_records dispatch starts the next batch size); the first launch of each
+batch is dropped and each counter is averaged over the rest.  Derived HBM bytes use the
+gfx950 FETCH_SIZE correction (x2 for wide streaming reads, MI355X_MICROARCH.md HBM)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(d, sizes):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+        disp = defaultdict(lambda: {"name": "", "c": defaultdict(float)})
+        for r in csv.DictReader(open(f)):
+            e = disp[int(r["Dispatch_Id"])]
+            e["name"] = r["Kernel_Name"]
+            e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
+        group, first = -1, False
+        for did in sorted(disp):
+            e = disp[did]
+            if "k_gen_records" in e["name"]:
+                group += 1
+                first = True
+                continue
+            if "k_verify_records" not in e["name"] or group < 0:
+                continue
+            if first:
+                first = False
+                continue
+            label = str(sizes[group]) if group < len(sizes) else f"batch{group}"
+            for c, v in e["c"].items():
+                acc[label][c].append(v)
+    out = {}
+    for label, cs in acc.items():
+        o = {c: sum(v) / len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in o:
+            o["hbm_read_bytes_per_launch"] = o["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in o:
+            o["hbm_write_bytes_per_launch"] = o["WRITE_SIZE"] * 1024
+        if "TCC_EA0_RDREQ_sum" in o:
+            o["ea_rd_bytes_if_64B_req"] = o["TCC_EA0_RDREQ_sum"] * 64
+        out[label] = o
+    print(json.dumps(out, indent=1))
+    json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1048576,16777216").split(",")])

@@ -194,6 +194,10 @@ int hfv_ctx_create(int device, hfv_ctx **out)
         }
         if (rc) break;
         if (query_geometry(device, &c->geom) != 0) { rc = -EIO; break; }
+        uint32_t *img = nullptr;
+        if (hipMalloc((void **)&img, 131072) != hipSuccess) { rc = -ENOMEM; break; }
+        c->geom.ttab_img = img;
+        if (build_ttab_image(img, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess) { rc = -EIO; break; }
     } while (0);
     if (rc) {
         hfv_ctx_destroy(c);
@@ -223,6 +227,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
     if (ctx->host_img) (void)hipHostFree(ctx->host_img);
+    if (ctx->geom.ttab_img) (void)hipFree((void *)ctx->geom.ttab_img);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -413,8 +418,8 @@ int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
     if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");
     const KernelVariant &a = ctx->geom.single, &b = ctx->geom.multi;
     snprintf(buf, len,
-             "zero: block=%d pf=%d tab=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d grid=%dx%d",
-             a.block, a.pf, a.tab, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab, ctx->geom.num_cus,
+             "zero: block=%d pf=%d tab=%d dma=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d dma=%d grid=%dx%d", a.block,
+             a.pf, a.tab, a.dma, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab, b.dma, ctx->geom.num_cus,
              b.blocks_per_cu);
     return 0;
 }

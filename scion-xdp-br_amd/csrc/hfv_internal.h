@@ -32,12 +32,14 @@ struct KernelVariant {
     int pf;              // record tiles loaded ahead of the one computed (1 or 2)
     int tab;             // round tables in LDS: 2 (T0/T1, 64 KiB) or 4 (T0..T3, 128 KiB)
     int blocks_per_cu;   // persistent grid = num_cus * blocks_per_cu
+    int dma;             // 1: fill the LDS tables from ttab_img by LDS-DMA; 0: compute them
 };
 
 struct LaunchGeom {
     int num_cus;
     KernelVariant single;   // KEYSEL_ZERO record verify
     KernelVariant multi;    // KEYSEL_IFID record verify (per-lane keys in LDS)
+    const uint32_t *ttab_img;   // 128 KiB device image of the replicated T0..T3 tables
 };
 
 // kernel launchers (hfv_kernels.hip); return hipError_t as int
@@ -53,6 +55,7 @@ int launch_expand_keys(const uint8_t *raw, size_t n, hop_key *out, DevKeyTable *
 int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
                        size_t n, uint64_t seed, uint64_t first_index, void *stream);
 int query_geometry(int device, LaunchGeom *g);
+int build_ttab_image(uint32_t *img, void *stream);
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);

@@ -77,6 +77,32 @@ __device__ __forceinline__ void fill_ttab()
     }
 }
 
+// Same table image copied from a prebuilt global copy (ctx->ttab_img, L2-resident after the
+// first blocks) by LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB per wave-instruction
+// straight into LDS, no VGPR round trip and ~16x fewer instructions than fill_ttab.
+template <int TAB>
+__device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
+{
+    constexpr int kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
+    for (int c = wave; c < kChunks; c += nw) {
+        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ void k_build_ttab_image(uint32_t *__restrict__ img)
+{
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 32768) return;
+    uint32_t t = c_t0[(e >> 6) & 255];
+    int rot = 8 * (((e >> 5) & 1) | ((e >> 13) & 2));
+    img[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
+}
+
 __device__ __forceinline__ void fill_keys(const DevKeyTable *tab)
 {
     const uint4 *src = reinterpret_cast<const uint4 *>(tab->rows);
@@ -89,7 +115,19 @@ __device__ __forceinline__ void fill_keys(const DevKeyTable *tab)
 // ---------------------------------------------------------------------------------------
 struct Lane {
     uint32_t b0, b1, b2, b3;   // LDS byte offsets of this lane's copies of T0..T3
+    uint32_t s0, s1, s2, s3;   // v_perm selectors SEL_B0..SEL_B3, held in VGPRs
+    uint32_t f01, f23;         // final-round byte-gather selectors
 };
+
+// Materialise a constant in a VGPR.  v_perm_b32 (VOP3 on gfx9) takes no literal, so its
+// selectors would otherwise occupy SGPRs; the SGPR-resident round keys already bring the
+// kernel close to the 80-SGPR line above which a SIMD holds fewer than 8 waves.
+__device__ __forceinline__ uint32_t vconst(uint32_t c)
+{
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
+    return r;
+}
 
 template <int TAB>
 __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const Lane &l)
@@ -98,15 +136,15 @@ __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const
     uint32_t n[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, SEL_B0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b1, SEL_B1);
+        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
+        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b1, l.s1);
         if constexpr (TAB == 4) {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, SEL_B2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, SEL_B3);
+            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, l.s2);
+            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, l.s3);
             n[c] = a ^ b ^ x ^ d ^ r[c];
         } else {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, SEL_B2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, SEL_B3);
+            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
+            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, l.s3);
             n[c] = a ^ b ^ r[c] ^ rot16(x ^ d);
         }
     }
@@ -121,15 +159,15 @@ __device__ __forceinline__ void round1_macinput(uint32_t s[4], const uint4 &rk1p
 {
     uint32_t n0, n1, n2, n3;
     if constexpr (TAB == 4) {
-        n0 = tlu<TAB>(s[1], l.b1, SEL_B1) ^ tlu<TAB>(s[2], l.b2, SEL_B2) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, SEL_B0) ^ tlu<TAB>(s[2], l.b1, SEL_B1) ^ tlu<TAB>(s[0], l.b3, SEL_B3) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, SEL_B1) ^ tlu<TAB>(s[0], l.b2, SEL_B2) ^ tlu<TAB>(s[1], l.b3, SEL_B3) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, SEL_B0) ^ tlu<TAB>(s[1], l.b2, SEL_B2) ^ tlu<TAB>(s[2], l.b3, SEL_B3) ^ rk1p.w;
+        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ tlu<TAB>(s[2], l.b2, l.s2) ^ rk1p.x;
+        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b3, l.s3) ^ rk1p.y;
+        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b2, l.s2) ^ tlu<TAB>(s[1], l.b3, l.s3) ^ rk1p.z;
+        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ tlu<TAB>(s[1], l.b2, l.s2) ^ tlu<TAB>(s[2], l.b3, l.s3) ^ rk1p.w;
     } else {
-        n0 = tlu<TAB>(s[1], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[2], l.b0, SEL_B2)) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, SEL_B0) ^ tlu<TAB>(s[2], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[0], l.b1, SEL_B3)) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, SEL_B1) ^ rot16(tlu<TAB>(s[0], l.b0, SEL_B2) ^ tlu<TAB>(s[1], l.b1, SEL_B3)) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, SEL_B0) ^ rot16(tlu<TAB>(s[1], l.b0, SEL_B2) ^ tlu<TAB>(s[2], l.b1, SEL_B3)) ^ rk1p.w;
+        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ rot16(tlu<TAB>(s[2], l.b0, l.s2)) ^ rk1p.x;
+        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b1, l.s3)) ^ rk1p.y;
+        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b0, l.s2) ^ tlu<TAB>(s[1], l.b1, l.s3)) ^ rk1p.z;
+        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ rot16(tlu<TAB>(s[1], l.b0, l.s2) ^ tlu<TAB>(s[2], l.b1, l.s3)) ^ rk1p.w;
     }
     s[0] = n0; s[1] = n1; s[2] = n2; s[3] = n3;
 }
@@ -141,11 +179,11 @@ __device__ __forceinline__ void round_last_full(uint32_t s[4], const uint4 &rk, 
     const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, SEL_B0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, SEL_B1);
-        uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, SEL_B2);
-        uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, SEL_B3);
-        out[c] = __builtin_amdgcn_perm(b, a, 0x0c0c0501u) ^ __builtin_amdgcn_perm(d, x, 0x05010c0cu) ^ r[c];
+        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
+        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, l.s1);
+        uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
+        uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, l.s3);
+        out[c] = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ r[c];
     }
 }
 
@@ -155,11 +193,11 @@ template <int TAB>
 __device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t &t0,
                                               uint32_t &t1)
 {
-    uint32_t a = tlu<TAB>(s[0], l.b0, SEL_B0), b = tlu<TAB>(s[1], l.b0, SEL_B1);
-    uint32_t x = tlu<TAB>(s[2], l.b0, SEL_B2), d = tlu<TAB>(s[3], l.b0, SEL_B3);
-    t0 = __builtin_amdgcn_perm(b, a, 0x0c0c0501u) ^ __builtin_amdgcn_perm(d, x, 0x05010c0cu) ^ rk.x;
-    uint32_t a1 = tlu<TAB>(s[1], l.b0, SEL_B0), b1 = tlu<TAB>(s[2], l.b0, SEL_B1);
-    t1 = __builtin_amdgcn_perm(b1, a1, 0x0c0c0501u) ^ rk.y;
+    uint32_t a = tlu<TAB>(s[0], l.b0, l.s0), b = tlu<TAB>(s[1], l.b0, l.s1);
+    uint32_t x = tlu<TAB>(s[2], l.b0, l.s2), d = tlu<TAB>(s[3], l.b0, l.s3);
+    t0 = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ rk.x;
+    uint32_t a1 = tlu<TAB>(s[1], l.b0, l.s0), b1 = tlu<TAB>(s[2], l.b0, l.s1);
+    t1 = __builtin_amdgcn_perm(b1, a1, l.f01) ^ rk.y;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -213,6 +251,8 @@ __device__ __forceinline__ Lane lane_bases()
 {
     uint32_t lane = threadIdx.x & 63;
     Lane l;
+    l.s0 = vconst(SEL_B0); l.s1 = vconst(SEL_B1); l.s2 = vconst(SEL_B2); l.s3 = vconst(SEL_B3);
+    l.f01 = vconst(0x0c0c0501u); l.f23 = vconst(0x05010c0cu);
     l.b0 = (lane & 31) << 2;
     l.b1 = l.b0 | 0x80u;
     l.b2 = l.b0 | 0x10000u;
@@ -293,8 +333,9 @@ __device__ __forceinline__ void verify_tile(const RecWords &cur, uint64_t t, uin
     if (lane == 0) bits[t] = ballot;
 }
 
-template <int KEYSEL, int BLOCK, int PF, int TAB>
+template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA>
 __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
+                                                          const uint32_t *__restrict__ ttab_img,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
                                                           uint64_t n, uint32_t inf_off, uint32_t hf_off,
                                                           uint64_t *__restrict__ bits)
@@ -307,7 +348,8 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
     const uint32_t nwaves = gridDim.x * kWaves;
 
-    fill_ttab<TAB>();
+    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
+    else fill_ttab<TAB>();
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
@@ -530,14 +572,16 @@ static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
     return (unsigned)(blocks ? blocks : 1);
 }
 
-using VerifyKernel = void (*)(const DevKeyTable *, const uint8_t *, uint64_t, uint64_t, uint32_t, uint32_t, uint64_t *);
+using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8_t *, uint64_t, uint64_t, uint32_t,
+                              uint32_t, uint64_t *);
 
 // Record-verify variants (tuning knobs; the default is chosen by scripts/sweep.py data).
 template <int KEYSEL>
 static VerifyKernel pick_verify(const KernelVariant &v)
 {
-#define HFV_V(B, P, T) \
-    if (v.block == B && v.pf == P && v.tab == T) return k_verify_records<KEYSEL, B, P, T>;
+#define HFV_V(B, P, T)                                                        \
+    if (v.block == B && v.pf == P && v.tab == T)                              \
+        return v.dma ? k_verify_records<KEYSEL, B, P, T, 1> : k_verify_records<KEYSEL, B, P, T, 0>;
     HFV_V(1024, 1, 2) HFV_V(1024, 2, 2) HFV_V(768, 1, 2) HFV_V(768, 2, 2) HFV_V(512, 1, 2) HFV_V(512, 2, 2)
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
         HFV_V(1024, 1, 4) HFV_V(1024, 2, 4) HFV_V(768, 1, 4) HFV_V(768, 2, 4) HFV_V(512, 1, 4) HFV_V(512, 2, 4)
@@ -555,7 +599,8 @@ int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     if (!k) return (int)hipErrorInvalidConfiguration;
     unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(v.block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, tab, recs, (uint64_t)stride, (uint64_t)n, inf_off, hf_off, bits);
+                          (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)stride,
+                          (uint64_t)n, inf_off, hf_off, bits);
     return (int)hipGetLastError();
 }
 
@@ -612,6 +657,7 @@ static void parse_variant(const char *env, KernelVariant *v)
         else if (sscanf(p, "pf=%d", &val) == 1) v->pf = val;
         else if (sscanf(p, "tab=%d", &val) == 1) v->tab = val;
         else if (sscanf(p, "bpc=%d", &val) == 1) v->blocks_per_cu = val;
+        else if (sscanf(p, "dma=%d", &val) == 1) v->dma = val;
         const char *c = strchr(p, ',');
         if (!c) break;
         p = c + 1;
@@ -635,14 +681,20 @@ static int finish_variant(int keysel, KernelVariant *v)
     return 0;
 }
 
+int build_ttab_image(uint32_t *img, void *stream)
+{
+    hipLaunchKernelGGL(k_build_ttab_image, dim3(128), dim3(256), 0, (hipStream_t)stream, img);
+    return (int)hipGetLastError();
+}
+
 int query_geometry(int device, LaunchGeom *g)
 {
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{768, 2, 2, 0};
-    g->multi = KernelVariant{1024, 2, 2, 0};
+    g->single = KernelVariant{768, 2, 2, 0, 1};
+    g->multi = KernelVariant{1024, 2, 2, 0, 1};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
     int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);

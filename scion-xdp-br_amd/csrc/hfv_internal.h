@@ -33,6 +33,7 @@ struct KernelVariant {
     int tab;             // round tables in LDS: 2 (T0/T1, 64 KiB) or 4 (T0..T3, 128 KiB)
     int blocks_per_cu;   // persistent grid = num_cus * blocks_per_cu
     int dma;             // 1: fill the LDS tables from ttab_img by LDS-DMA; 0: compute them
+    int np;              // packets per lane computed together (1 or 2)
 };
 
 struct LaunchGeom {

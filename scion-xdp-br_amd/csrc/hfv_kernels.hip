@@ -312,28 +312,58 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
     return t0 == e0 && ((t1 ^ e1) & 0xffffu) == 0;
 }
 
-// One tile = 64 consecutive records = one wave.  PF tiles are loaded ahead of the one being
-// computed, so the loads of tile t + PF*nwaves overlap the AES rounds of tile t.
-template <int KEYSEL, int TAB>
-__device__ __forceinline__ void verify_tile(const RecWords &cur, uint64_t t, uint64_t n, uint32_t lane, const Lane &l,
-                                            const UniformKey *ukey, uint64_t *__restrict__ bits)
+// One tile = 64 consecutive records = one wave.  A wave computes NP tiles at once (NP
+// independent AES chains per lane, interleaved by the scheduler to hide LDS latency), and
+// loads its next NP tiles while it computes the current ones (PF = prefetch depth in
+// iterations).  Tiles of one wave: t, t + nwaves, t + 2*nwaves, ...
+template <int KEYSEL, int TAB, int NP>
+__device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t t, uint64_t nwaves, uint64_t n,
+                                             uint32_t lane, const Lane &l, const UniformKey *ukey,
+                                             uint64_t *__restrict__ bits)
 {
-    uint32_t w[4], t0, t1;
-    rec_macinput(cur, w);
-    bool ok = t * 64 + lane < n;
-    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        cmac48_macinput<TAB>(w, *ukey, l, t0, t1);
-    } else {
-        const LdsKey key(rec_key_slot(cur));
-        cmac48_macinput<TAB>(w, key, l, t0, t1);
-        ok = ok && key.ok();
+    uint32_t s[NP][4];
+    uint32_t slot[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        uint32_t w[4];
+        rec_macinput(cur[p], w);
+        slot[p] = rec_key_slot(cur[p]);
+        uint4 k0;
+        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) k0 = ukey->row(0);
+        else k0 = LdsKey(slot[p]).row(0);
+        s[p][0] = w[0] ^ k0.x; s[p][1] = w[1] ^ k0.y; s[p][2] = w[2] ^ k0.z; s[p][3] = w[3] ^ k0.w;
     }
-    bool pass = ok && rec_tag_matches(cur, t0, t1);
-    uint64_t ballot = __ballot(pass);
-    if (lane == 0) bits[t] = ballot;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round1_macinput<TAB>(s[p], ukey->row(11), l);
+        else round1_macinput<TAB>(s[p], LdsKey(slot[p]).row(11), l);
+    }
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round_full<TAB>(s[p], ukey->row(r), l);
+            else round_full<TAB>(s[p], LdsKey(slot[p]).row(r), l);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        uint32_t t0, t1;
+        bool ok = (t + p * nwaves) * 64 + lane < n;
+        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+            round_last_48<TAB>(s[p], ukey->row(10), l, t0, t1);
+        } else {
+            const LdsKey key(slot[p]);
+            round_last_48<TAB>(s[p], key.row(10), l, t0, t1);
+            ok = ok && key.ok();
+        }
+        bool pass = ok && rec_tag_matches(cur[p], t0, t1);
+        uint64_t ballot = __ballot(pass);
+        if (lane == 0 && t + p * nwaves < (n + 63) / 64) bits[t + p * nwaves] = ballot;
+    }
 }
 
-template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA>
+template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP>
 __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
                                                           const uint32_t *__restrict__ ttab_img,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
@@ -341,12 +371,13 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
                                                           uint64_t *__restrict__ bits)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
+    static_assert(NP == 1 || NP == 2, "packets per lane");
     static_assert(KEYSEL == HFV_KEYSEL_ZERO || TAB == 2, "per-lane keys need the 64 KiB table layout");
     constexpr uint32_t kWaves = BLOCK / 64;
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
-    const uint32_t nwaves = gridDim.x * kWaves;
+    const uint64_t nwaves = gridDim.x * kWaves;
 
     if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
     else fill_ttab<TAB>();
@@ -365,21 +396,30 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
         ukp = &ukey;
     }
     const uint64_t last = n - 1;
+    const uint64_t step = NP * nwaves;   // tiles consumed per iteration by the whole grid
     uint64_t t = wave;
-    RecWords cur = load_rec(recs, stride, t * 64 + lane, last, inf_off, hf_off);
-    if constexpr (PF == 1) {
-        for (; t < ntiles; t += nwaves) {
-            RecWords nx1 = load_rec(recs, stride, (t + nwaves) * 64 + lane, last, inf_off, hf_off);
-            verify_tile<KEYSEL, TAB>(cur, t, n, lane, l, ukp, bits);
-            cur = nx1;
-        }
-    } else {
-        RecWords nx1 = load_rec(recs, stride, (t + nwaves) * 64 + lane, last, inf_off, hf_off);
-        for (; t < ntiles; t += nwaves) {
-            RecWords nx2 = load_rec(recs, stride, (t + 2 * nwaves) * 64 + lane, last, inf_off, hf_off);
-            verify_tile<KEYSEL, TAB>(cur, t, n, lane, l, ukp, bits);
-            cur = nx1;
-            nx1 = nx2;
+    RecWords cur[NP], nx1[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) cur[p] = load_rec(recs, stride, (t + p * nwaves) * 64 + lane, last, inf_off, hf_off);
+    if constexpr (PF == 2) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+            nx1[p] = load_rec(recs, stride, (t + step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
+    }
+    for (; t < ntiles; t += step) {
+        RecWords nxt[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+            nxt[p] = load_rec(recs, stride, (t + PF * step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
+        verify_tiles<KEYSEL, TAB, NP>(cur, t, nwaves, n, lane, l, ukp, bits);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if constexpr (PF == 2) {
+                cur[p] = nx1[p];
+                nx1[p] = nxt[p];
+            } else {
+                cur[p] = nxt[p];
+            }
         }
     }
 }
@@ -579,12 +619,13 @@ using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8
 template <int KEYSEL>
 static VerifyKernel pick_verify(const KernelVariant &v)
 {
-#define HFV_V(B, P, T)                                                        \
-    if (v.block == B && v.pf == P && v.tab == T)                              \
-        return v.dma ? k_verify_records<KEYSEL, B, P, T, 1> : k_verify_records<KEYSEL, B, P, T, 0>;
-    HFV_V(1024, 1, 2) HFV_V(1024, 2, 2) HFV_V(768, 1, 2) HFV_V(768, 2, 2) HFV_V(512, 1, 2) HFV_V(512, 2, 2)
+#define HFV_V(B, P, T)                                                                          \
+    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 1, 1>; \
+    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 2) return k_verify_records<KEYSEL, B, P, T, 1, 2>; \
+    if (v.block == B && v.pf == P && v.tab == T && !v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 0, 1>;
+    HFV_V(1024, 1, 2) HFV_V(1024, 2, 2) HFV_V(768, 1, 2) HFV_V(512, 1, 2)
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        HFV_V(1024, 1, 4) HFV_V(1024, 2, 4) HFV_V(768, 1, 4) HFV_V(768, 2, 4) HFV_V(512, 1, 4) HFV_V(512, 2, 4)
+        HFV_V(1024, 1, 4) HFV_V(768, 1, 4)
     }
 #undef HFV_V
     return nullptr;
@@ -658,6 +699,7 @@ static void parse_variant(const char *env, KernelVariant *v)
         else if (sscanf(p, "tab=%d", &val) == 1) v->tab = val;
         else if (sscanf(p, "bpc=%d", &val) == 1) v->blocks_per_cu = val;
         else if (sscanf(p, "dma=%d", &val) == 1) v->dma = val;
+        else if (sscanf(p, "np=%d", &val) == 1) v->np = val;
         const char *c = strchr(p, ',');
         if (!c) break;
         p = c + 1;
@@ -693,8 +735,8 @@ int query_geometry(int device, LaunchGeom *g)
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{768, 2, 2, 0, 1};
-    g->multi = KernelVariant{1024, 2, 2, 0, 1};
+    g->single = KernelVariant{1024, 1, 2, 0, 1, 1};
+    g->multi = KernelVariant{1024, 1, 2, 0, 1, 1};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
     int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);

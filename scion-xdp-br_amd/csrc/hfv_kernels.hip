@@ -91,6 +91,9 @@ __device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                          (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
     }
+    // vmcnt retires in issue order; the DMA pieces are the youngest loads, and the record
+    // loads issued before them must complete as well before the barrier (the compiler
+    // inserts that wait anyway), so a full drain is the correct and only wait here.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -379,22 +382,8 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
     const uint64_t nwaves = gridDim.x * kWaves;
 
-    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
-    else fill_ttab<TAB>();
-    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
-    __syncthreads();
-    const Lane l = lane_bases();
-
-    const UniformKey *ukp = nullptr;
-    UniformKey ukey(tab);
-    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
-            for (uint64_t t = wave; t < ntiles; t += nwaves)
-                if (lane == 0) bits[t] = 0;
-            return;
-        }
-        ukp = &ukey;
-    }
+    // First tiles' record loads go out before the table fill so the fill overlaps their
+    // memory latency.
     const uint64_t last = n - 1;
     const uint64_t step = NP * nwaves;   // tiles consumed per iteration by the whole grid
     uint64_t t = wave;
@@ -405,6 +394,23 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
 #pragma unroll
         for (int p = 0; p < NP; ++p)
             nx1[p] = load_rec(recs, stride, (t + step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
+    }
+    UniformKey ukey(tab);
+
+    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
+    else fill_ttab<TAB>();
+    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
+    __syncthreads();
+    const Lane l = lane_bases();
+
+    const UniformKey *ukp = nullptr;
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+        if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
+            for (uint64_t tt = wave; tt < ntiles; tt += nwaves)
+                if (lane == 0) bits[tt] = 0;
+            return;
+        }
+        ukp = &ukey;
     }
     for (; t < ntiles; t += step) {
         RecWords nxt[NP];

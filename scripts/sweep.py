@@ -76,7 +76,24 @@ def main():
                     ctx.verify_records(recs, n, bits, stream=sh)
                 torch.cuda.synchronize()
                 wall = (time.perf_counter() - t0) / 100
+                # two streams, two independent batches alternating (BR pipeline shape)
+                recs2 = torch.empty_like(recs)
+                recs2.copy_(recs)
+                bits2 = torch.zeros_like(bits)
+                s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(100):
+                    if i & 1:
+                        ctx.verify_records(recs2, n, bits2, stream=s2.cuda_stream)
+                    else:
+                        ctx.verify_records(recs, n, bits, stream=s1.cuda_stream)
+                torch.cuda.synchronize()
+                wall2 = (time.perf_counter() - t0) / 100
+                assert popcount(bits2) == expected_pass_count(n, 0)
+                del recs2, bits2
                 out[f"n={n} {keysel} {v}"] = {
+                    "b2b_2stream_wall_us": round(wall2 * 1e6, 2), "b2b_2stream_mpkts": round(n / wall2 / 1e6, 1),
                     "kernel_us_med": round(med * 1e3, 2), "kernel_us_min": round(ts[0] * 1e3, 2),
                     "kernel_mpkts": round(n / med / 1e3, 1), "alg_GBs": round(n * 64.125 / med / 1e6, 1),
                     "b2b_wall_us": round(wall * 1e6, 2), "b2b_mpkts": round(n / wall / 1e6, 1),

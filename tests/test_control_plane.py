@@ -1,0 +1,63 @@
+"""Control plane without a GPU: the pinned key map and the hfv-loader CLI behave like
+`br-loader key add|remove` on the bpffs-pinned mac_key_map (br/src/br_loader.cpp:182-261)."""
+import os
+import subprocess
+
+import pytest
+
+import orc
+import scion_hfv as hfv
+
+LOADER = os.path.join(hfv.PKG_ROOT, "bin", "hfv-loader")
+
+
+@pytest.fixture()
+def pin_dir(tmp_path, monkeypatch):
+    monkeypatch.setenv("HFV_PIN_DIR", str(tmp_path))
+    return tmp_path
+
+
+def run(*args, env=None):
+    return subprocess.run([LOADER, *args], capture_output=True, text=True, env=env)
+
+
+def test_keymap_update_erase_read(pin_dir):
+    path = hfv.keymap_path("br1")
+    assert path == os.path.join(str(pin_dir), "br1", "mac_key_map")
+    hk = orc.hop_key(orc.KEY_1111)
+    hfv.keymap_update(path, 0, hk)
+    hfv.keymap_update(path, 200, orc.hop_key(b"2222222222222222"))
+    slots = hfv.keymap_read(path)
+    assert sorted(slots) == [0, 200] and slots[0] == hk
+    hfv.keymap_erase(path, 200)
+    assert sorted(hfv.keymap_read(path)) == [0]
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_erase(path, 200)          # erase of a missing element fails
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_update(path, 256, hk)     # out of range
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_path("../etc")
+
+
+def test_cli_matches_br_loader_semantics(pin_dir):
+    if not os.path.exists(LOADER):
+        pytest.skip("hfv-loader not built")
+    env = dict(os.environ)
+    r = run("key", "add", "br1", "0", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert r.returncode == 0, r.stderr
+    r = run("key", "add", "br1", "3", "MjIyMjIyMjIyMjIyMjIyMg==", env=env)
+    assert r.returncode == 0
+    slots = hfv.keymap_read(hfv.keymap_path("br1"))
+    assert slots[0] == orc.hop_key(orc.KEY_1111)            # expansion + K1 like br_loader.cpp:213-218
+    assert slots[3] == orc.hop_key(b"2222222222222222")
+    listing = run("key", "list", "br1", env=env).stdout.split()
+    assert listing[0] == "0" and listing[1] == "K1=21bf836becd9fad43b88dacd20f7dd62"
+    assert run("key", "remove", "br1", "3", env=env).returncode == 0
+    bad = run("key", "remove", "br1", "3", env=env)
+    assert bad.returncode != 0 and "Update failed" in bad.stderr
+    bad = run("key", "add", "br1", "zz", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert bad.returncode != 0 and "Invalid verification key index" in bad.stderr
+    bad = run("key", "add", "br1", "1", "MTEx", env=env)
+    assert bad.returncode != 0 and "Invalid MAC verification key" in bad.stderr
+    bad = run("key", env=env)
+    assert bad.returncode != 0 and "Usage" in bad.stderr

@@ -1,5 +1,7 @@
 """Parity of the MI355X kernels (through the C ABI) against the CPU checker and the
 committed reference fixtures.  Integer work: every comparison is bit-exact."""
+import os
+
 import numpy as np
 import pytest
 
@@ -13,7 +15,7 @@ DEV = "cuda:0"
 
 
 def dev(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return torch.from_numpy(np.array(a, copy=True)).to(DEV)
 
 
 def host(t):
@@ -250,3 +252,29 @@ def test_empty_and_bad_arguments(ctx):
         ctx.verify_records(recs, 4, bits, stride=40)        # HF beyond the stride
     with pytest.raises(hfv.HfvError):
         ctx.set_keysel(7)
+
+
+def test_pinned_keymap_attach(ctx, tmp_path, monkeypatch):
+    """A data plane attached to the pinned map sees `hfv-loader key add/remove` from another
+    process at its next batch (reusePinnedMap + RCU-like update, br_loader.cpp:119-126)."""
+    import subprocess
+    monkeypatch.setenv("HFV_PIN_DIR", str(tmp_path))
+    loader = os.path.join(hfv.PKG_ROOT, "bin", "hfv-loader")
+    path = hfv.keymap_path("br1")
+    ctx.attach_keymap(path)                       # creates an empty map
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    bits = new_bits(n)
+    ctx.verify_records(d, n, bits)
+    assert not bits_np(bits, n).any()
+    assert subprocess.run([loader, "key", "add", "br1", "0", "MTExMTExMTExMTExMTExMQ=="]).returncode == 0
+    ctx.verify_records(d, n, bits)
+    assert np.array_equal(bits_np(bits, n), g["pass_bits"])
+    assert subprocess.run([loader, "key", "remove", "br1", "0"]).returncode == 0
+    ctx.verify_records(d, n, bits)
+    assert not bits_np(bits, n).any()
+    ctx.key_add(0, orc.KEY_1111)                  # write-through from the attached ctx
+    assert hfv.keymap_read(path)[0] == orc.hop_key(orc.KEY_1111)
+    ctx.verify_records(d, n, bits)
+    assert np.array_equal(bits_np(bits, n), g["pass_bits"])

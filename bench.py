@@ -88,6 +88,16 @@ def kernel_ms(ctx, recs, n, bits, stream, reps):
     return float(np.mean(ts)), float(ts[len(ts) // 2])
 
 
+def pmc_traffic(keysel, n):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (scripts/pmc_round.sh) for this
+    exact configuration, committed in profiles/traffic.json; None if not measured."""
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        return json.load(open(tpath))[f"{keysel}:{n}"]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
 def cpu_baseline(recs_host, keysel, gpu_bits, budget_s):
     """The reference aes.c soft path (XDP's arithmetic) timed on this host's cores over a
     bounded sample of the same records; verdicts must equal the GPU's."""
@@ -184,16 +194,7 @@ def main():
     bytes_per_launch = hfv.BYTES_PER_PACKET * n
     achieved = bytes_per_launch / (k_mean * 1e-3) / 1e9
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            key = f"{args.keysel}:{n}"
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(args.keysel, n)
 
     result = {
         "metric": "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets",
@@ -232,7 +233,8 @@ def main():
         bm, bmed = kernel_ms(ctx, big, nb, bbits, stream, 20)
         ach = hfv.BYTES_PER_PACKET * nb / (bm * 1e-3) / 1e9
         result["hbm_resident"] = {"records": nb, "kernel_ms_mean": round(bm, 4), "mpkts": round(nb / bm / 1e3, 1),
-                                  "achieved_GBs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
+                                  "achieved_GBs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                                  "traffic": pmc_traffic(args.keysel, nb)}
         del big, bbits
 
     if rank == 0 and world == 1 and not args.no_host_e2e:

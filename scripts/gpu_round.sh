@@ -28,7 +28,8 @@ if [[ $MODE == all || $MODE == bench ]]; then
     step bench 600 python bench.py || exit $?
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
+    # the same command as the bench step, under the kernel tracer
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-        python3 bench.py --steps 50 --warmup 5 --big-n 0 --cpu-budget 0 --no-host-e2e || exit $?
-    find $OUT/prof -name "*stats*.csv" | head
+        python3 bench.py || exit $?
+    python3 scripts/prof_summary.py $OUT/prof/run_kernel_trace.csv $OUT/prof/verify_by_batch.json
 fi

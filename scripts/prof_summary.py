@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Per-batch summary of a rocprofv3 --kernel-trace of bench.py: verify launches are grouped
+by the k_gen_records dispatch that precedes them (one per batch size), so the mean verify
+duration per batch size can be compared with bench.py's roofline.kernel_ms_mean."""
+import csv
+import json
+import sys
+
+
+def main(trace_csv, out_json):
+    rows = sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
+    groups, cur = [], None
+    for r in rows:
+        name = r["Kernel_Name"]
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        if "k_gen_records" in name:
+            cur = {"after_gen_grid": int(r.get("Grid_Size_X", r.get("Grid_Size", 0))), "verify_us": []}
+            groups.append(cur)
+        elif "k_verify_records" in name and cur is not None:
+            cur["verify_us"].append(dur)
+    out = []
+    for g in groups:
+        v = sorted(g["verify_us"])
+        if not v:
+            continue
+        out.append({"launches": len(v), "mean_us": round(sum(v) / len(v), 3), "median_us": round(v[len(v) // 2], 3),
+                    "min_us": round(v[0], 3), "max_us": round(v[-1], 3)})
+    json.dump(out, open(out_json, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -193,7 +193,10 @@ int hfv_ctx_create(int device, hfv_ctx **out)
             if (hipEventCreateWithFlags(&c->tab_done[i], hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
         }
         if (rc) break;
-        if (query_geometry(device, &c->geom) != 0) { rc = -EIO; break; }
+        if (query_geometry(device, &c->geom) != 0) {
+            hfv_ctx_destroy(c);
+            return fail(-EINVAL, "no kernel variant matches HFV_KVARIANT / HFV_KVARIANT_IFID");
+        }
         uint32_t *img = nullptr;
         if (hipMalloc((void **)&img, 131072) != hipSuccess) { rc = -ENOMEM; break; }
         c->geom.ttab_img = img;

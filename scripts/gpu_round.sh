@@ -21,7 +21,7 @@ if [[ $MODE == all || $MODE == test ]]; then
     step pytest_gpu 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider
     rc=$?; [[ $rc -gt 1 ]] && exit $rc
 fi
-if [[ $MODE == all || $MODE == sweep ]]; then
+if [[ $MODE == sweep ]]; then
     step sweep 600 python scripts/sweep.py ${SWEEP_ARGS:-} || exit $?
 fi
 if [[ $MODE == all || $MODE == bench ]]; then

@@ -22,9 +22,8 @@ import scion_hfv as hfv  # noqa: E402
 sys.path.insert(0, ROOT)
 from bench import KEY_1111, SEED_RECORDS, key_table_256, expected_pass_count, popcount  # noqa: E402
 
-ZERO = ("block=1024,pf=1,tab=2;block=1024,pf=2,tab=2;block=768,pf=1,tab=2;block=768,pf=2,tab=2;"
-        "block=512,pf=2,tab=2;block=1024,pf=2,tab=4;block=768,pf=2,tab=4;block=512,pf=2,tab=4")
-IFID = "block=1024,pf=2,tab=2;block=768,pf=2,tab=2;block=512,pf=2,tab=2"
+ZERO = "block=1024,pf=1,tab=2,bpc=1;block=1024,pf=1,tab=2,bpc=2;block=768,pf=1,tab=2;block=1024,pf=1,tab=4"
+IFID = "block=1024,pf=1,tab=2;block=768,pf=1,tab=2"
 
 
 def make(keysel, variant):

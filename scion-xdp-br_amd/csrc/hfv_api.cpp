@@ -416,6 +416,24 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
     return 0;
 }
 
+// Diagnostic (not part of include/scion_hfv.h): the default KEYSEL_ZERO kernel with per-wave
+// s_memrealtime stamps, for the timeline analysis in scripts/stamps.py.  stamps: device
+// buffer of (grid * 16 waves) x 16 u64; returns the grid size in *grid.
+extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n, uint64_t *pass_bits,
+                                        uint64_t *stamps, void *stream, int *grid)
+{
+    if (!ctx || !recs || !pass_bits || !stamps || !grid || n == 0) return fail(-EINVAL, "bad argument");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevKeyTable *tab;
+    int rc = publish_keys(ctx, st, &tab);
+    if (rc) return rc;
+    uint64_t tiles = (n + 63) / 64, blocks = (tiles + 15) / 16, cap = (uint64_t)ctx->geom.num_cus * ctx->geom.single.blocks_per_cu;
+    *grid = (int)(blocks < cap ? blocks : cap);
+    int e = launch_verify_stamped(ctx->geom, tab, (const uint8_t *)recs, n, pass_bits, stamps, st);
+    return after_launch(ctx, st, e, "stamped launch");
+}
+
 int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
 {
     if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");

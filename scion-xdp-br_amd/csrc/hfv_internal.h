@@ -56,6 +56,8 @@ int launch_expand_keys(const uint8_t *raw, size_t n, hop_key *out, DevKeyTable *
 int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
                        size_t n, uint64_t seed, uint64_t first_index, void *stream);
 int query_geometry(int device, LaunchGeom *g);
+int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
+                          uint64_t *bits, uint64_t *stamps, void *stream);
 int build_ttab_image(uint32_t *img, void *stream);
 
 // pinned key map (hfv_keymap.cpp)

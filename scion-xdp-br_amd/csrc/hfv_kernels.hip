@@ -366,12 +366,15 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
     }
 }
 
-template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP>
+// STAMP = 1 is a diagnostic build: lane 0 of every wave records s_memrealtime (100 MHz,
+// chip-wide) at entry, after the table fill, after each of its first 12 tiles and at exit
+// into stamps[wave * 16 + k].  Nothing else reads the stamps.
+template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP, int STAMP = 0>
 __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
                                                           const uint32_t *__restrict__ ttab_img,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
                                                           uint64_t n, uint32_t inf_off, uint32_t hf_off,
-                                                          uint64_t *__restrict__ bits)
+                                                          uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     static_assert(NP == 1 || NP == 2, "packets per lane");
@@ -381,6 +384,11 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
     const uint64_t nwaves = gridDim.x * kWaves;
+    uint64_t *st = STAMP ? stamps + (uint64_t)wave * 16 : nullptr;
+    int nst = 0;
+    if constexpr (STAMP) {
+        if (lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+    }
 
     // First tiles' record loads go out before the table fill so the fill overlaps their
     // memory latency.
@@ -402,6 +410,9 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
+    if constexpr (STAMP) {
+        if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+    }
 
     const UniformKey *ukp = nullptr;
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
@@ -418,6 +429,10 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
         for (int p = 0; p < NP; ++p)
             nxt[p] = load_rec(recs, stride, (t + PF * step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
         verify_tiles<KEYSEL, TAB, NP>(cur, t, nwaves, n, lane, l, ukp, bits);
+        if constexpr (STAMP) {
+            if (lane == 0 && nst < 12) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
+            ++nst;
+        }
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             if constexpr (PF == 2) {
@@ -427,6 +442,9 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
                 cur[p] = nxt[p];
             }
         }
+    }
+    if constexpr (STAMP) {
+        if (lane == 0) st[15] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -619,7 +637,7 @@ static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
 }
 
 using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8_t *, uint64_t, uint64_t, uint32_t,
-                              uint32_t, uint64_t *);
+                              uint32_t, uint64_t *, uint64_t *);
 
 // Record-verify variants (tuning knobs; the default is chosen by scripts/sweep.py data).
 template <int KEYSEL>
@@ -647,7 +665,18 @@ int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(v.block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)stride,
-                          (uint64_t)n, inf_off, hf_off, bits);
+                          (uint64_t)n, inf_off, hf_off, bits, (uint64_t *)nullptr);
+    return (int)hipGetLastError();
+}
+
+int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
+                          uint64_t *bits, uint64_t *stamps, void *stream)
+{
+    const KernelVariant &v = g.single;
+    unsigned grid = grid_for(n, 1024, g.num_cus, v.blocks_per_cu);
+    hipLaunchKernelGGL((k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1>), dim3(grid), dim3(1024), 0,
+                       (hipStream_t)stream, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)64, (uint64_t)n,
+                       (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits, stamps);
     return (int)hipGetLastError();
 }
 

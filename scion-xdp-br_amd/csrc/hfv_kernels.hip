@@ -444,7 +444,12 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
         }
     }
     if constexpr (STAMP) {
-        if (lane == 0) st[15] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            st[15] = __builtin_amdgcn_s_memrealtime();
+            // placement: HW_REG_HW_ID (hwreg 4, all 32 bits) and HW_REG_XCC_ID (hwreg 20)
+            st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                     ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+        }
     }
 }
 

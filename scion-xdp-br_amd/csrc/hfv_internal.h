@@ -34,6 +34,7 @@ struct KernelVariant {
     int blocks_per_cu;   // persistent grid = num_cus * blocks_per_cu
     int dma;             // 1: fill the LDS tables from ttab_img by LDS-DMA; 0: compute them
     int np;              // packets per lane computed together (1 or 2)
+    int dyn;             // 1: waves pull tiles from a per-block LDS queue; 0: static stride
 };
 
 struct LaunchGeom {

@@ -46,6 +46,7 @@ __shared__ uint32_t s_tab64[16384];
 __shared__ uint32_t s_tab128[32768];
 __shared__ uint4 s_keys[kDevKeyRows * HFV_MAX_KEYS];   // 48 KiB, round-major
 __shared__ uint32_t s_valid[8];
+__shared__ uint32_t s_next_tile;   // DYN: the block's tile queue head
 
 // v_perm selector for state byte k: address byte 0 <- base byte 0 (copy + T0/T1 bit),
 // byte 1 <- state byte k, byte 2 <- base byte 2 (T2/T3 bit), byte 3 <- 0.
@@ -369,7 +370,71 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
 // STAMP = 1 is a diagnostic build: lane 0 of every wave records s_memrealtime (100 MHz,
 // chip-wide) at entry, after the table fill, after each of its first 12 tiles and at exit
 // into stamps[wave * 16 + k].  Nothing else reads the stamps.
-template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP, int STAMP = 0>
+// Dynamic variant: block b owns the contiguous tile range [b*T/G, (b+1)*T/G) and its waves
+// pull tiles from an LDS counter, so waves that the LDS arbiter serves less often simply
+// take fewer tiles instead of finishing last (static assignment left the last ~20 % of the
+// kernel with few waves active: scripts/stamps.py).  A wave claims its next tile before
+// computing the current one, so the next tile's record loads still overlap the rounds.
+template <int KEYSEL, int BLOCK, int TAB, int DMA, int STAMP>
+__device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ tab,
+                                               const uint32_t *__restrict__ ttab_img,
+                                               const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
+                                               uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
+                                               uint64_t *__restrict__ st)
+{
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t b0 = ntiles * blockIdx.x / gridDim.x, b1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    const uint32_t count = (uint32_t)(b1 - b0);
+    const uint64_t last = n - 1;
+    const uint32_t kWaves = BLOCK / 64;
+    // first tile of each wave is static (wave index); the queue hands out the rest
+    uint32_t t = wave_uniform(threadIdx.x / 64);
+    RecWords cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+    UniformKey ukey(tab);
+    if (threadIdx.x == 0) s_next_tile = kWaves;
+    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
+    else fill_ttab<TAB>();
+    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
+    __syncthreads();
+    const Lane l = lane_bases();
+    int nst = 0;
+    if constexpr (STAMP) {
+        if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    const UniformKey *ukp = nullptr;
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+        if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
+            for (uint32_t tt = t; tt < count; tt += kWaves)
+                if (lane == 0) bits[b0 + tt] = 0;
+            return;
+        }
+        ukp = &ukey;
+    }
+    while (t < count) {
+        uint32_t nt = 0;
+        if (lane == 0) nt = atomicAdd(&s_next_tile, 1u);
+        nt = wave_uniform(nt);
+        RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
+        RecWords c1[1] = {cur};
+        verify_tiles<KEYSEL, TAB, 1>(c1, b0 + t, 0, n, lane, l, ukp, bits);
+        if constexpr (STAMP) {
+            if (lane == 0 && nst < 12) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
+            ++nst;
+        }
+        cur = nxt;
+        t = nt;
+    }
+    if constexpr (STAMP) {
+        if (lane == 0) {
+            st[15] = __builtin_amdgcn_s_memrealtime();
+            st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                     ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+        }
+    }
+}
+
+template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP, int STAMP = 0, int DYN = 0>
 __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
                                                           const uint32_t *__restrict__ ttab_img,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
@@ -390,6 +455,10 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
         if (lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
     }
 
+    if constexpr (DYN) {
+        verify_dynamic<KEYSEL, BLOCK, TAB, DMA, STAMP>(tab, ttab_img, recs, stride, n, inf_off, hf_off, bits, st);
+        return;
+    }
     // First tiles' record loads go out before the table fill so the fill overlaps their
     // memory latency.
     const uint64_t last = n - 1;
@@ -649,6 +718,8 @@ template <int KEYSEL>
 static VerifyKernel pick_verify(const KernelVariant &v)
 {
 #define HFV_V(B, P, T)                                                                          \
+    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1 && v.dyn)                        \
+        return k_verify_records<KEYSEL, B, P, T, 1, 1, 0, 1>;                                           \
     if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 1, 1>; \
     if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 2) return k_verify_records<KEYSEL, B, P, T, 1, 2>; \
     if (v.block == B && v.pf == P && v.tab == T && !v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 0, 1>;
@@ -679,7 +750,9 @@ int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uin
 {
     const KernelVariant &v = g.single;
     unsigned grid = grid_for(n, 1024, g.num_cus, v.blocks_per_cu);
-    hipLaunchKernelGGL((k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1>), dim3(grid), dim3(1024), 0,
+    auto k = v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 1>
+                   : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 0>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(1024), 0,
                        (hipStream_t)stream, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)64, (uint64_t)n,
                        (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits, stamps);
     return (int)hipGetLastError();
@@ -740,6 +813,7 @@ static void parse_variant(const char *env, KernelVariant *v)
         else if (sscanf(p, "bpc=%d", &val) == 1) v->blocks_per_cu = val;
         else if (sscanf(p, "dma=%d", &val) == 1) v->dma = val;
         else if (sscanf(p, "np=%d", &val) == 1) v->np = val;
+        else if (sscanf(p, "dyn=%d", &val) == 1) v->dyn = val;
         const char *c = strchr(p, ',');
         if (!c) break;
         p = c + 1;
@@ -775,8 +849,8 @@ int query_geometry(int device, LaunchGeom *g)
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{1024, 1, 2, 1, 1, 1};
-    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1};
+    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 0};
+    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 0};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
     int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);

@@ -67,9 +67,9 @@ def main():
         hwid = (hw & np.uint64(0xffffffff)).astype(np.int64)
         xcc = ((hw >> np.uint64(32)) & np.uint64(0xf)).astype(np.int64)
         cu = (hwid >> 8) & 0xf
-        sh = (hwid >> 12) & 1
+        shv = (hwid >> 12) & 1
         se = (hwid >> 13) & 0x7
-        cu_key = xcc * 1000 + se * 100 + sh * 16 + cu
+        cu_key = xcc * 1000 + se * 100 + shv * 16 + cu
         life = (s[:, 15] - s[:, 0]) * TICK_US
         endt = (s[:, 15] - t0) * TICK_US
         uniq, counts = np.unique(cu_key, return_counts=True)
@@ -79,7 +79,7 @@ def main():
             if m.any():
                 print(f"  xcc {x}: waves {int(m.sum())} end p50 {np.median(endt[m]):.2f} max {endt[m].max():.2f} life p50 {np.median(life[m]):.2f}")
         slow = np.argsort(endt)[-20:]
-        print("  slowest waves (xcc,se,sh,cu,end):", [(int(xcc[i]), int(se[i]), int(sh[i]), int(cu[i]), round(float(endt[i]), 2)) for i in slow[-8:]])
+        print("  slowest waves (xcc,se,sh,cu,end):", [(int(xcc[i]), int(se[i]), int(shv[i]), int(cu[i]), round(float(endt[i]), 2)) for i in slow[-8:]])
         per_cu_end = {k: endt[cu_key == k].max() for k in uniq}
         v = np.array(sorted(per_cu_end.values()))
         print(f"  per-CU last-wave end: p10 {v[len(v)//10]:.2f} p50 {v[len(v)//2]:.2f} p90 {v[9*len(v)//10]:.2f} max {v[-1]:.2f}")

@@ -849,8 +849,8 @@ int query_geometry(int device, LaunchGeom *g)
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 0};
-    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 0};
+    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 1};
+    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 1};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
     int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);

@@ -154,6 +154,78 @@ int hfv_key_add_batch(hfv_ctx *ctx, uint32_t first, const struct aes_key *keys, 
 int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t seed, uint64_t first_index,
                     void *stream);
 
+/* ---- full BR per-packet path (config 4) -------------------------------------------------
+ * border_router / process_packet (br/src/bpf/xdp.c:54-284) over a batch of Ethernet frames:
+ * parse Eth/IPv4|IPv6/UDP/SCION (parser.h), AS ingress/egress processing with deferred HF
+ * verification (path_processing.h), next-hop resolution, rewrite with incremental IP/UDP
+ * checksums (rewrite.h), HF MAC verification (slot 0 of the ctx key table, xdp.c:259-274),
+ * redirect decision and per-ingress-interface verdict counters (record_verdict).
+ *
+ * The BPF maps become one configuration struct.  bpf_fib_lookup (a kernel helper) is
+ * replaced by a static next-hop table with longest-prefix match; an address with no route
+ * behaves like BPF_FIB_LKUP_RET_NOT_FWDED.  Addresses and ports are in wire byte order. */
+#define HFV_AF_INET 2
+#define HFV_AF_INET6 10
+#define HFV_BR_MAX_IFACES 16
+#define HFV_BR_MAX_ROUTES 64
+#define HFV_BR_MAX_TXPORTS 128
+#define HFV_BR_COUNTERS 11         /* enum counter (common.h:40-53) */
+#define HFV_BR_STATS_IFINDEX 64    /* counters kept for ingress ifindex < 64 */
+
+struct hfv_br_int_iface {          /* int_iface_map: ifindex -> internal address (common.h:116-128) */
+    uint32_t ifindex;
+    uint32_t family;
+    uint8_t addr[16];              /* IPv4 in addr[0..3] */
+    uint8_t port[2];
+    uint8_t pad[2];
+};
+struct hfv_br_ingress {            /* ingress_map: {dst addr, dst port, ifindex} -> AS interface id (common.h:73-84) */
+    uint32_t ifindex;
+    uint32_t family;
+    uint8_t addr[16];
+    uint8_t port[2];
+    uint8_t pad[2];
+    uint32_t ifid;
+};
+struct hfv_br_egress {             /* egress_map: ifid -> fwd_info (common.h:131-145) */
+    uint32_t ifid;
+    uint32_t fwd_external;         /* 1: ext_link {remote, local}, 0: sibling BR {remote = its internal address} */
+    uint32_t family;
+    uint8_t remote[16];
+    uint8_t local[16];
+    uint8_t remote_port[2];
+    uint8_t local_port[2];
+};
+struct hfv_br_route {              /* replaces bpf_fib_lookup (fib_lookup.h:74-261) */
+    uint32_t family;
+    uint8_t prefix[16];
+    uint32_t prefix_len;
+    int32_t ret;                   /* BPF_FIB_LKUP_RET_*: 0 success, 1-3 drop, 4-8 pass */
+    uint32_t ifindex;
+    uint8_t smac[6];
+    uint8_t dmac[6];
+};
+struct hfv_br_config {
+    uint32_t n_int_ifaces, n_ingress, n_egress, n_routes, n_tx_ports;
+    struct hfv_br_int_iface int_ifaces[HFV_BR_MAX_IFACES];
+    struct hfv_br_ingress ingress[HFV_BR_MAX_IFACES];
+    struct hfv_br_egress egress[HFV_BR_MAX_IFACES];
+    struct hfv_br_route routes[HFV_BR_MAX_ROUTES];
+    uint32_t tx_ports[HFV_BR_MAX_TXPORTS];   /* tx_port_map: ifindices a redirect may target */
+};
+
+/* Install the router tables (copied; takes effect for batches enqueued afterwards). */
+int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
+/* Process n frames in place.  pkts: frame i at pkts + i*slot (slot % 8 == 0, >= 64);
+ * len[i] its length (<= slot); ingress_ifindex[i] the receiving interface.  Outputs per
+ * frame: action[i] = the XDP action returned (0 aborted, 1 drop, 2 pass, 4 redirect),
+ * verdict[i] = the last enum verdict recorded, egress_ifindex[i] = redirect target or -1.
+ * stats (nullable): u64 [HFV_BR_STATS_IFINDEX][2][HFV_BR_COUNTERS] (bytes, packets) to which
+ * the batch's record_verdict calls are added.  All pointers are device pointers. */
+int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex,
+                   size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats,
+                   void *stream);
+
 /* ---- host helpers ---------------------------------------------------------------------- */
 /* Scalar verify_hop_field on the host (SURVEY.md 8b v) for control-plane checks. */
 int hfv_verify_macinput(const struct macinput *mi, uint64_t expected, const struct hop_key *key);

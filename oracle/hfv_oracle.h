@@ -85,6 +85,13 @@ void orc_gen_key_table(uint64_t seed, uint32_t nkeys, uint8_t keys[][16]);
 void orc_gen_records(uint8_t *recs, size_t stride, size_t n, uint64_t seed, uint64_t first_index,
                      const orc_hop_key *keys, int keysel);
 
+/* ---- full BR per-packet path (config 4), hfv_br_oracle.c -------------------------------- */
+/* cfg: struct hfv_br_config (include/scion_hfv.h); key0: mac_key_map[0] or NULL.  Same
+ * outputs as hfv_br_process; stats may be NULL. */
+void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                    const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                    int32_t *egress_ifindex, uint64_t *stats);
+
 #ifdef __cplusplus
 }
 #endif

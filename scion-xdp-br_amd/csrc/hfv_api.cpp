@@ -56,6 +56,72 @@ struct DeviceGuard {
     }
 };
 
+// ---- router tables (hfv_br_set_config) -------------------------------------------------
+static uint32_t le32(const uint8_t *q) { return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24; }
+static uint32_t be32(const uint8_t *q) { return (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | (uint32_t)q[3]; }
+static uint32_t le16(const uint8_t *q) { return (uint32_t)q[0] | (uint32_t)q[1] << 8; }
+
+void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
+{
+    memset(out, 0, sizeof *out);
+    out->n_int = in->n_int_ifaces;
+    out->n_ing = in->n_ingress;
+    out->n_egr = in->n_egress;
+    out->n_routes = in->n_routes;
+    for (uint32_t i = 0; i < in->n_int_ifaces; ++i) {
+        const hfv_br_int_iface &a = in->int_ifaces[i];
+        DevBrIntIface &d = out->int_ifaces[i];
+        d.ifindex = a.ifindex;
+        d.family = a.family;
+        for (int w = 0; w < 4; ++w) d.addr[w] = le32(a.addr + 4 * w);
+        d.port = le16(a.port);
+    }
+    for (uint32_t i = 0; i < in->n_ingress; ++i) {   // struct ingress_addr key layout, common.h:73-84
+        const hfv_br_ingress &a = in->ingress[i];
+        DevBrIngress &d = out->ingress[i];
+        if (a.family == HFV_AF_INET) d.v4 = le32(a.addr);
+        else
+            for (int w = 0; w < 4; ++w) d.v6[w] = le32(a.addr + 4 * w);
+        d.port = le16(a.port);
+        d.ifindex16 = a.ifindex & 0xffffu;
+        d.ifid = a.ifid;
+    }
+    for (uint32_t i = 0; i < in->n_egress; ++i) {
+        const hfv_br_egress &a = in->egress[i];
+        DevBrEgress &d = out->egress[i];
+        d.ifid = a.ifid;
+        d.fwd_external = a.fwd_external;
+        d.family = a.family;
+        for (int w = 0; w < 4; ++w) {
+            d.remote[w] = le32(a.remote + 4 * w);
+            d.local[w] = le32(a.local + 4 * w);
+            d.remote_be[w] = be32(a.remote + 4 * w);
+        }
+        d.remote_port = le16(a.remote_port);
+        d.local_port = le16(a.local_port);
+    }
+    for (uint32_t i = 0; i < in->n_routes; ++i) {
+        const hfv_br_route &a = in->routes[i];
+        DevBrRoute &d = out->routes[i];
+        uint32_t width = a.family == HFV_AF_INET ? 32 : a.family == HFV_AF_INET6 ? 128 : 0;
+        d.family = (width && a.prefix_len <= width) ? a.family : 0;
+        d.plen = a.prefix_len;
+        for (int w = 0; w < 4; ++w) {
+            uint32_t lo = 32u * (uint32_t)w, bits = a.prefix_len > lo ? a.prefix_len - lo : 0;
+            d.mask[w] = bits >= 32 ? 0xffffffffu : bits ? ~0u << (32 - bits) : 0u;
+            d.pfx[w] = be32(a.prefix + 4 * w) & d.mask[w];
+        }
+        d.ret = a.ret;
+        d.ifindex = a.ifindex;
+        d.dmac_lo = le32(a.dmac);
+        d.dmac_hi = le16(a.dmac + 4);
+        d.smac_lo = le32(a.smac);
+        d.smac_hi = le16(a.smac + 4);
+    }
+    for (uint32_t i = 0; i < in->n_tx_ports; ++i)
+        if (in->tx_ports[i] < HFV_BR_MAX_TXPORTS) out->tx_bits[in->tx_ports[i] >> 5] |= 1u << (in->tx_ports[i] & 31);
+}
+
 }  // namespace hfv
 
 using namespace hfv;
@@ -71,9 +137,9 @@ struct hfv_ctx {
     uint32_t valid[8] = {0};
     bool dirty = true;
     // publication
-    DevKeyTable *host_img = nullptr;      // pinned staging image
+    DevState *host_img = nullptr;         // pinned staging image
     hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
-    DevKeyTable *dev_tab[2] = {nullptr, nullptr};
+    DevState *dev_tab[2] = {nullptr, nullptr};
     hipEvent_t tab_done[2] = {nullptr, nullptr};   // scratch events for the reader fence
     hipStream_t readers[2][8] = {};                // streams that launched with dev_tab[i]
     int nreaders[2] = {0, 0};
@@ -92,6 +158,8 @@ struct hfv_ctx {
     char keymap_path[4096] = {0};
     // dispatch timing (hfv_verify_records_timed)
     hipEvent_t tev[2] = {nullptr, nullptr};
+    // router tables for hfv_br_process (published with the key table)
+    DevBrConfig br{};
 };
 
 // NULL is HIP's default stream, as for any HIP API taking a stream.
@@ -103,7 +171,7 @@ static hipStream_t pick_stream(hfv_ctx *, void *stream) { return (hipStream_t)st
 static void note_reader(hfv_ctx *ctx, hipStream_t st);
 
 // Make the shadow table visible to work enqueued next on `st`; returns the table to use.
-static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
+static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
 {
     if (ctx->keymap) {   // pick up updates other processes made to the pinned map
         uint32_t seq = keymap_seq(ctx->keymap);
@@ -120,9 +188,10 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
             uint32_t dk[4 * kDevKeyRows];
             if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) compile_dev_key(&ctx->shadow[k], dk);
             else memset(dk, 0, sizeof dk);
-            for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->rows[r][k], dk + 4 * r, 16);
+            for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->keys.rows[r][k], dk + 4 * r, 16);
         }
-        memcpy(ctx->host_img->valid, ctx->valid, sizeof ctx->valid);
+        memcpy(ctx->host_img->keys.valid, ctx->valid, sizeof ctx->valid);
+        ctx->host_img->br = ctx->br;
         // the device table may only be overwritten after every launch that read it completed
         if (ctx->readers_overflow[next]) {
             HIP_TRY(hipDeviceSynchronize());
@@ -136,7 +205,7 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevKeyTable **out)
         }
         ctx->nreaders[next] = 0;
         ctx->readers_overflow[next] = false;
-        HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevKeyTable), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
         ctx->dirty = false;
@@ -185,11 +254,11 @@ int hfv_ctx_create(int device, hfv_ctx **out)
     int rc = 0;
     do {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = -EIO; break; }
-        if (hipHostMalloc((void **)&c->host_img, sizeof(DevKeyTable), hipHostMallocDefault) != hipSuccess) { rc = -ENOMEM; break; }
+        if (hipHostMalloc((void **)&c->host_img, sizeof(DevState), hipHostMallocDefault) != hipSuccess) { rc = -ENOMEM; break; }
         if (hipEventCreateWithFlags(&c->img_free, hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
         for (int i = 0; i < 2; ++i) {
-            if (hipMalloc((void **)&c->dev_tab[i], sizeof(DevKeyTable)) != hipSuccess) { rc = -ENOMEM; break; }
-            if (hipMemset(c->dev_tab[i], 0, sizeof(DevKeyTable)) != hipSuccess) { rc = -EIO; break; }
+            if (hipMalloc((void **)&c->dev_tab[i], sizeof(DevState)) != hipSuccess) { rc = -ENOMEM; break; }
+            if (hipMemset(c->dev_tab[i], 0, sizeof(DevState)) != hipSuccess) { rc = -EIO; break; }
             if (hipEventCreateWithFlags(&c->tab_done[i], hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
         }
         if (rc) break;
@@ -381,9 +450,10 @@ int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
         return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
     DeviceGuard g(ctx->device);
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
                                   ctx->hf_off, pass_bits, st);
     return after_launch(ctx, st, e, "verify_records launch");
@@ -404,9 +474,10 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
     for (int i = 0; i < 2; ++i)
         if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
                                   ctx->hf_off, pass_bits, st, ctx->tev[0], ctx->tev[1]);
     rc = after_launch(ctx, st, e, "verify_records launch");
@@ -425,9 +496,10 @@ extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n
     if (!ctx || !recs || !pass_bits || !stamps || !grid || n == 0) return fail(-EINVAL, "bad argument");
     DeviceGuard g(ctx->device);
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     uint64_t tiles = (n + 63) / 64, blocks = (tiles + 15) / 16, cap = (uint64_t)ctx->geom.num_cus * ctx->geom.single.blocks_per_cu;
     *grid = (int)(blocks < cap ? blocks : cap);
     int e = launch_verify_stamped(ctx->geom, tab, (const uint8_t *)recs, n, pass_bits, stamps, st);
@@ -456,9 +528,10 @@ int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t
         return fail(-EINVAL, "macinputs must be 16-byte aligned, expected/bitmap 8-byte aligned");
     DeviceGuard g(ctx->device);
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     int e = launch_verify_macinputs(ctx->geom, tab, mi, expected, key_index, n, pass_bits, st);
     return after_launch(ctx, st, e, "verify_macinputs launch");
 }
@@ -472,9 +545,10 @@ int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_in
     if (((uintptr_t)mi & 15) || ((uintptr_t)tags & 15)) return fail(-EINVAL, "macinputs/tags must be 16-byte aligned");
     DeviceGuard g(ctx->device);
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     int e = launch_cmac_tags(ctx->geom, tab, mi, key_index, n, tags, st);
     return after_launch(ctx, st, e, "cmac_tags launch");
 }
@@ -503,11 +577,55 @@ int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t 
         return fail(-EINVAL, "the generator writes the default 64 B layout only");
     DeviceGuard g(ctx->device);
     hipStream_t st = pick_stream(ctx, stream);
-    DevKeyTable *tab;
-    int rc = publish_keys(ctx, st, &tab);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
+    const DevKeyTable *tab = &ds->keys;
     int e = launch_gen_records(ctx->geom, tab, ctx->keysel, (uint8_t *)recs, stride, n, seed, first_index, st);
     return after_launch(ctx, st, e, "gen_records launch");
+}
+
+// ---- full border-router path (config 4) ---------------------------------------------------
+
+int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
+{
+    if (!ctx || !cfg) return fail(-EINVAL, "null argument");
+    if (cfg->n_int_ifaces > HFV_BR_MAX_IFACES || cfg->n_ingress > HFV_BR_MAX_IFACES ||
+        cfg->n_egress > HFV_BR_MAX_IFACES || cfg->n_routes > HFV_BR_MAX_ROUTES || cfg->n_tx_ports > HFV_BR_MAX_TXPORTS)
+        return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
+                    HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
+    compile_br_config(cfg, &ctx->br);
+    ctx->dirty = true;
+    return 0;
+}
+
+static int br_args(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex,
+                   uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (!pkts || !len || !ingress_ifindex || !action || !verdict || !egress_ifindex) return fail(-EINVAL, "null buffer");
+    if (slot < 64 || (slot & 7) || ((uintptr_t)pkts & 7)) return fail(-EINVAL, "slot must be >= 64 and a multiple of 8, frames 8-byte aligned");
+    if (((uintptr_t)len & 1) || ((uintptr_t)ingress_ifindex & 3) || ((uintptr_t)egress_ifindex & 3))
+        return fail(-EINVAL, "misaligned length/ifindex array");
+    return 0;
+}
+
+int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex,
+                   size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats,
+                   void *stream)
+{
+    if (n == 0) return ctx ? 0 : fail(-EINVAL, "ctx is NULL");
+    int rc = br_args(ctx, pkts, slot, len, ingress_ifindex, action, verdict, egress_ifindex);
+    if (rc) return rc;
+    if ((uintptr_t)stats & 7) return fail(-EINVAL, "misaligned stats");
+    DeviceGuard g(ctx->device);
+    hipStream_t st = pick_stream(ctx, stream);
+    DevState *ds;
+    rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_br_process(ctx->geom, ds, pkts, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex,
+                              stats, st);
+    return after_launch(ctx, st, e, "br_process launch");
 }
 
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
@@ -551,9 +669,10 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         size_t first = c * chunk, cnt = n - first < chunk ? n - first : chunk;
         memcpy(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, cnt * stride);
         HIP_TRY(hipMemcpyAsync(ctx->d_rec[slot], ctx->h_pin[slot], cnt * stride, hipMemcpyHostToDevice, st));
-        DevKeyTable *tab;
-        int rc = publish_keys(ctx, st, &tab);
+        DevState *ds;
+        int rc = publish_keys(ctx, st, &ds);
         if (rc) return rc;
+        const DevKeyTable *tab = &ds->keys;
         int e = launch_verify_records(ctx->geom, tab, ctx->keysel, ctx->d_rec[slot], stride, cnt, ctx->inf_off,
                                       ctx->hf_off, ctx->d_bits[slot], st);
         rc = after_launch(ctx, st, e, "verify_records launch");

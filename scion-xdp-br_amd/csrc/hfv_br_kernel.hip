@@ -1,0 +1,600 @@
+// hfv_br_kernel.hip -- the reference XDP border router's whole per-packet path (config 4) on
+// gfx950: parse Ethernet/IPv4|IPv6/UDP/SCION, AS ingress/egress hop processing, next-hop
+// lookup, in-place rewrite with incremental checksums, deferred hop-field AES-CMAC check,
+// redirect decision and verdict counters.
+//
+// Follows, function by function:
+//   border_router / process_packet / record_verdict / verify_hop_field  br/src/bpf/xdp.c:54-284
+//   parse_underlay / parse_scion / parse_scion_path                      br/src/bpf/parser.h:45-204
+//   defer_verify_hop_field / scion_as_ingress / scion_as_egress          br/src/bpf/path_processing.h:39-152
+//   fib_lookup_as_egress / fib_lookup_egress_br / fib_lookup_ip_forward  br/src/bpf/fib_lookup.h:29-261
+//   rewrite / rewrite_scion_path                                         br/src/bpf/rewrite.h:35-146
+// with the reference's quirks kept (listed in oracle/hfv_br_oracle.c, the CPU checker).
+// bpf_fib_lookup is replaced by the static next-hop table of the installed hfv_br_config.
+//
+// Mapping: one lane per frame, a persistent grid with one 1024-thread block per CU.  Each
+// block stages the AES round tables (64 KiB, LDS-DMA from the ctx image), the router tables
+// (~10 KiB) and its verdict counters (11 KiB) in LDS.  Frames are read and patched in place in
+// HBM through byte loads/stores of just the header fields the parser touches; payload bytes
+// are never read.  At most one hop field is checked per frame (ingress from a neighbour AS
+// or egress of a packet from the own AS), with the record-verify kernel's AES code (slot-0
+// key in SGPRs, conflict-free replicated T-tables).
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include "hfv_aes_dev.h"
+#include "hfv_internal.h"
+
+namespace hfv {
+
+static __shared__ DevBrConfig s_br;
+static __shared__ unsigned long long s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+
+// enum xdp_action and enum verdict (br/src/bpf/common.h:38-70)
+enum : uint32_t { A_ABORTED = 0, A_DROP = 1, A_PASS = 2, A_TX = 3, A_REDIRECT = 4 };
+constexpr uint32_t verd(uint32_t action, uint32_t counter) { return (action & 7u) | (counter << 3); }
+enum : uint32_t {
+    V_ABORT = verd(A_ABORTED, 0), V_FORWARD = verd(A_REDIRECT, 1), V_PARSE_ERROR = verd(A_DROP, 2),
+    V_NOT_SCION = verd(A_PASS, 3), V_NOT_IMPLEMENTED = verd(A_PASS, 4), V_NO_INTERFACE = verd(A_DROP, 5),
+    V_UNDERLAY_MISMATCH = verd(A_PASS, 6), V_ROUTER_ALERT = verd(A_PASS, 7), V_FIB_DROP = verd(A_DROP, 8),
+    V_FIB_PASS = verd(A_PASS, 9), V_INVALID_HF = verd(A_DROP, 10)
+};
+
+// The BPF code reads and writes network-order fields through little-endian u16/u32 views.
+__device__ __forceinline__ uint32_t g8(const uint8_t *q) { return q[0]; }
+__device__ __forceinline__ uint32_t g16(const uint8_t *q) { return (uint32_t)q[0] | ((uint32_t)q[1] << 8); }
+__device__ __forceinline__ uint32_t g32(const uint8_t *q)
+{
+    return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+}
+__device__ __forceinline__ void p16(uint8_t *q, uint32_t v) { q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); }
+__device__ __forceinline__ void p32(uint8_t *q, uint32_t v)
+{
+    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+}
+__device__ __forceinline__ uint32_t sw16(uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); }
+__device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(v); }
+
+// Per-frame state: struct headers + the per-CPU scratchpad (common.h:154-225), zeroed per frame.
+struct BrFrame {
+    uint8_t *p;
+    int len;
+    uint32_t ifindex;
+    uint32_t last_verdict;
+    int ip, udp, meta, inf, hf;
+    uint32_t verdict;
+    uint32_t family;
+    uint32_t v4_dst, v4_src, v4_ttl;
+    uint32_t v6_dst[4], v6_src[4], v6_hop;
+    uint32_t udp_dst, udp_src;
+    uint32_t path_type, h_meta, curr_inf, curr_hf;
+    uint32_t seg_id0, seg_id1;
+    uint32_t segment_switch, seg0, num_inf, num_hf;
+    uint64_t ip_residual, udp_residual;
+    uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;
+    int egress_ifindex;
+    // deferred MAC check: ingress (mask bit 0) and egress-from-internal (bit 1) never both apply
+    bool need_mac;
+    uint32_t mi[4];
+    uint32_t mac_lo, mac_hi;
+};
+
+template <bool STATS>
+__device__ __forceinline__ uint32_t record(BrFrame &k, uint32_t verdict)   // record_verdict, xdp.c:54-70
+{
+    uint32_t idx = (verdict >> 3) & 0x0fu;
+    k.last_verdict = verdict;
+    if constexpr (STATS) {
+        if (k.ifindex < HFV_BR_STATS_IFINDEX && idx < HFV_BR_COUNTERS) {
+            unsigned long long *row = s_stats + k.ifindex * 2 * HFV_BR_COUNTERS;
+            atomicAdd(row + idx, (unsigned long long)k.len);
+            atomicAdd(row + HFV_BR_COUNTERS + idx, 1ull);
+        }
+    }
+    return verdict & 7u;
+}
+
+// ---- parser.h ----------------------------------------------------------------------------
+__device__ __forceinline__ int parse_underlay(BrFrame &k)
+{
+    k.verdict = V_NOT_SCION;
+    int off = 14;
+    if (off > k.len) return -1;
+    uint32_t proto = g16(k.p + 12);
+    if (proto == 0x0008u) {   // ETH_P_IP, network order
+        k.ip = off;
+        off += 20;
+        if (off > k.len) return -1;
+        const uint8_t *ip = k.p + k.ip;
+        k.family = HFV_AF_INET;
+        k.v4_dst = g32(ip + 16);
+        k.ip_residual -= k.v4_dst;
+        k.v4_src = g32(ip + 12);
+        k.ip_residual -= k.v4_src;
+        k.udp_residual = k.ip_residual;
+        k.v4_ttl = g8(ip + 8);
+        k.ip_residual -= k.v4_ttl;
+        int skip = 4 * (int)(g8(ip) & 0x0fu) - 20;
+        if (skip < 0 || skip > 40) return -1;
+        off += skip;
+        if (g8(ip + 9) != 17u) return -1;
+    } else if (proto == 0xdd86u) {   // ETH_P_IPV6
+        k.ip = off;
+        off += 40;
+        if (off > k.len) return -1;
+        const uint8_t *ip = k.p + k.ip;
+        k.family = HFV_AF_INET6;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            k.v6_dst[i] = g32(ip + 24 + 4 * i);
+            k.udp_residual -= k.v6_dst[i];
+            k.v6_src[i] = g32(ip + 8 + 4 * i);
+            k.udp_residual -= k.v6_src[i];
+        }
+        k.v6_hop = g8(ip + 7);
+        if (g8(ip + 6) != 17u) return -1;
+    } else {
+        return -1;
+    }
+    k.udp = off;
+    off += 8;
+    if (off > k.len) return -1;
+    k.udp_dst = g16(k.p + k.udp + 2);
+    k.udp_residual -= k.udp_dst;
+    k.udp_src = g16(k.p + k.udp);
+    k.udp_residual -= k.udp_src;
+    return off;
+}
+
+__device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
+{
+    k.verdict = V_PARSE_ERROR;
+    k.meta = off;
+    off += 4;
+    if (off > k.len) return -1;
+    uint32_t raw = g32(k.p + k.meta);
+    k.udp_residual -= raw;
+    k.h_meta = sw32(raw);
+    k.seg0 = (k.h_meta >> 12) & 0x3fu;
+    uint32_t seg1 = (k.h_meta >> 6) & 0x3fu, seg2 = k.h_meta & 0x3fu;
+    k.num_inf = (k.seg0 > 0) + (seg1 > 0) + (seg2 > 0);
+    k.num_hf = k.seg0 + seg1 + seg2;
+    k.curr_inf = (k.h_meta >> 30) & 0x03u;
+    k.curr_hf = (k.h_meta >> 24) & 0x3fu;
+    int inf = off + (int)k.curr_inf * 8;
+    k.inf = inf;
+    if (inf + 8 > k.len) return -1;
+    k.seg_id0 = g16(k.p + inf + 2);
+    k.udp_residual -= k.seg_id0;
+    if (k.curr_inf + 1 < k.num_inf) {
+        inf += 8;
+        if (inf + 8 > k.len) return -1;
+        k.seg_id1 = g16(k.p + inf + 2);
+    }
+    k.hf = off + (int)k.num_inf * 8 + (int)k.curr_hf * 12;
+    if (k.hf + 12 > k.len) return -1;
+    return off;
+}
+
+__device__ __forceinline__ int parse_scion(BrFrame &k, int off)
+{
+    k.verdict = V_PARSE_ERROR;
+    int sc = off;
+    off += 28;
+    if (off > k.len) return -1;
+    if ((g8(k.p + sc) >> 4) != 0) {
+        k.verdict = V_NOT_IMPLEMENTED;
+        return -1;
+    }
+    uint32_t haddr = g8(k.p + sc + 9);
+    off += 8 + 4 * (int)((haddr >> 2) & 0x2u) + 4 * (int)((haddr >> 6) & 0x2u);   // SC_GET_DL/SL, scion.h:49-52
+    if (off > k.len) return -1;
+    k.path_type = g8(k.p + sc + 8);
+    if (k.path_type == 1u) return parse_scion_path(k, off);
+    k.verdict = V_NOT_IMPLEMENTED;
+    return -1;
+}
+
+// ---- path_processing.h ---------------------------------------------------------------------
+__device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return g8(k.p + inf) & 1u; }
+
+__device__ __forceinline__ void defer_verify(BrFrame &k, int inf, int hf, uint32_t beta_nbo)
+{
+    k.need_mac = true;
+    k.mi[0] = (beta_nbo & 0xffffu) << 16;
+    k.mi[1] = g32(k.p + inf + 4);
+    k.mi[2] = (g8(k.p + hf + 1) << 8) | (g16(k.p + hf + 2) << 16);
+    k.mi[3] = g16(k.p + hf + 4);
+    k.mac_lo = g32(k.p + hf + 6);
+    k.mac_hi = g16(k.p + hf + 10);
+}
+
+__device__ __forceinline__ bool as_ingress(BrFrame &k)
+{
+    const uint8_t *hf = k.p + k.hf;
+    if (g8(hf) & 0x03u) {
+        k.verdict = V_ROUTER_ALERT;
+        return false;
+    }
+    uint32_t c = cons_at(k, k.inf);
+    uint32_t beta = sw16(k.seg_id0);
+    if (!c) beta ^= g8(hf + 7) | (g8(hf + 6) << 8);
+    defer_verify(k, k.inf, k.hf, sw16(beta));
+    if (!c) k.seg_id0 = sw16(beta);
+    uint32_t seg_end = k.seg0;   // path_processing.h:84-86 adds seg0 for every index
+    if (k.curr_inf >= 1) seg_end += k.seg0;
+    if (k.curr_inf >= 2) seg_end += k.seg0;
+    uint32_t next_hf = k.curr_hf + 1;
+    if (next_hf >= k.num_hf) {
+        k.verdict = V_NOT_IMPLEMENTED;
+        return false;
+    }
+    if (next_hf == seg_end) {
+        k.segment_switch = 1;
+        ++k.curr_inf;
+        ++k.curr_hf;
+        k.hf += 12;
+        if (k.hf + 12 > k.len) {
+            k.verdict = V_PARSE_ERROR;
+            return false;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
+{
+    k.verdict = A_ABORTED;
+    const uint8_t *hf = k.p + k.hf;
+    if (g8(hf) & 0x03u) {
+        k.verdict = V_ROUTER_ALERT;
+        return false;
+    }
+    int inf = k.inf;
+    if (k.segment_switch) {
+        inf += 8;
+        if (inf + 8 > k.len) return false;
+    }
+    uint32_t beta = sw16(k.segment_switch ? k.seg_id1 : k.seg_id0);
+    if (as_ing_ifid == 0) defer_verify(k, k.inf, k.hf, sw16(beta));   // original INF, path_processing.h:142
+    if (cons_at(k, inf)) {
+        uint32_t nb = sw16((beta ^ (g8(hf + 7) | (g8(hf + 6) << 8))) & 0xffffu);
+        if (k.segment_switch) k.seg_id1 = nb;
+        else k.seg_id0 = nb;
+    }
+    ++k.curr_hf;
+    return true;
+}
+
+// ---- tables (LDS) ----------------------------------------------------------------------------
+__device__ __forceinline__ int int_iface(uint32_t ifindex)
+{
+    for (uint32_t i = 0; i < s_br.n_int; ++i)
+        if (s_br.int_ifaces[i].ifindex == ifindex) return (int)i;
+    return -1;
+}
+
+__device__ __forceinline__ int ingress_lookup(const BrFrame &k)
+{
+    for (uint32_t i = 0; i < s_br.n_ing; ++i) {
+        const DevBrIngress &e = s_br.ingress[i];
+        if (e.v4 == k.v4_dst && e.v6[0] == k.v6_dst[0] && e.v6[1] == k.v6_dst[1] && e.v6[2] == k.v6_dst[2] &&
+            e.v6[3] == k.v6_dst[3] && e.port == k.udp_dst && e.ifindex16 == (k.ifindex & 0xffffu))
+            return (int)i;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int egress_lookup(uint32_t ifid)
+{
+    for (uint32_t i = 0; i < s_br.n_egr; ++i)
+        if (s_br.egress[i].ifid == ifid) return (int)i;
+    return -1;
+}
+
+// longest-prefix match on (family, destination as big-endian words); ties keep the first entry
+__device__ __forceinline__ int route_lookup(uint32_t family, const uint32_t dst_be[4])
+{
+    int best = -1;
+    uint32_t best_len = 0;
+    for (uint32_t i = 0; i < s_br.n_routes; ++i) {
+        const DevBrRoute &r = s_br.routes[i];
+        if (r.family != family) continue;
+        uint32_t diff = ((dst_be[0] ^ r.pfx[0]) & r.mask[0]) | ((dst_be[1] ^ r.pfx[1]) & r.mask[1]) |
+                        ((dst_be[2] ^ r.pfx[2]) & r.mask[2]) | ((dst_be[3] ^ r.pfx[3]) & r.mask[3]);
+        if (diff == 0 && (best < 0 || r.plen > best_len)) {
+            best = (int)i;
+            best_len = r.plen;
+        }
+    }
+    return best;
+}
+
+// bpf_fib_lookup return-code handling shared by the fib_lookup_* helpers; false = stop
+__device__ __forceinline__ bool fib_result(BrFrame &k, int r)
+{
+    int ret = r >= 0 ? s_br.routes[r].ret : 4;   // no route: BPF_FIB_LKUP_RET_NOT_FWDED
+    if (ret >= 1 && ret <= 3) {
+        k.verdict = V_FIB_DROP;
+        return false;
+    }
+    if (ret >= 4 && ret <= 8) {
+        k.verdict = V_FIB_PASS;
+        return false;
+    }
+    if (r >= 0) {
+        const DevBrRoute &e = s_br.routes[r];
+        k.dmac_lo = e.dmac_lo; k.dmac_hi = e.dmac_hi;
+        k.smac_lo = e.smac_lo; k.smac_hi = e.smac_hi;
+    } else {
+        k.dmac_lo = k.dmac_hi = k.smac_lo = k.smac_hi = 0;
+    }
+    return true;
+}
+
+__device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link)
+{
+    k.udp_dst = link.remote_port;
+    k.udp_src = link.local_port;
+    if (k.family == HFV_AF_INET) {
+        k.v4_dst = link.remote[0];
+        k.v4_src = link.local[0];
+        k.v4_ttl = 64;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            k.v6_dst[i] = link.remote[i];
+            k.v6_src[i] = link.local[i];
+        }
+        k.v6_hop = 64;
+    }
+    int r = route_lookup(k.family, link.remote_be);
+    if (!fib_result(k, r)) return -1;
+    return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
+}
+
+__device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
+{
+    k.udp_dst = sib.remote_port;
+    if (k.family == HFV_AF_INET) {
+        k.v4_dst = sib.remote[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) k.v6_dst[i] = sib.remote[i];
+    }
+    int r = route_lookup(k.family, sib.remote_be);
+    if (!fib_result(k, r)) return -1;
+    uint32_t out_if = r >= 0 ? s_br.routes[r].ifindex : 0;
+    int s = int_iface(out_if);
+    if (s < 0) {
+        k.verdict = V_ABORT;
+        return -1;
+    }
+    const DevBrIntIface &src = s_br.int_ifaces[s];
+    if (src.family != k.family) {
+        k.verdict = V_UNDERLAY_MISMATCH;
+        return -1;
+    }
+    k.udp_src = src.port;
+    if (k.family == HFV_AF_INET) {
+        k.v4_src = src.addr[0];
+        k.v4_ttl = 64;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) k.v6_src[i] = src.addr[i];
+        k.v6_hop = 64;
+    }
+    return (int)out_if;
+}
+
+__device__ __forceinline__ int fib_ip_forward(BrFrame &k)
+{
+    uint32_t dst[4];
+    if (k.family == HFV_AF_INET) {
+        dst[0] = sw32(g32(k.p + k.ip + 16));   // hdr->ip.v4->daddr
+        dst[1] = dst[2] = dst[3] = 0;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[i] = sw32(k.v6_dst[i]);
+    }
+    int r = route_lookup(k.family, dst);
+    if (!fib_result(k, r)) return -1;
+    k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
+    return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
+}
+
+// ---- rewrite.h -------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fold_checksum(uint64_t c)
+{
+    c = (c & 0xffffu) + (c >> 16);
+    c = (c & 0xffffu) + (c >> 16);
+    c = ~c;
+    if (c == 0) c = 0xffff;
+    return (uint32_t)(c & 0xffffu);
+}
+
+__device__ __forceinline__ void rewrite(BrFrame &k)
+{
+    uint8_t *p = k.p;
+    p32(p, k.dmac_lo); p16(p + 4, k.dmac_hi);
+    p32(p + 6, k.smac_lo); p16(p + 10, k.smac_hi);
+    if (k.family == HFV_AF_INET) {
+        uint8_t *ip = p + k.ip;
+        p32(ip + 16, k.v4_dst);
+        p32(ip + 12, k.v4_src);
+        uint64_t c = (uint64_t)k.v4_dst + (uint64_t)k.v4_src;
+        k.ip_residual += c;
+        k.udp_residual += c;
+        ip[8] = (uint8_t)k.v4_ttl;
+        k.ip_residual += k.v4_ttl;
+        uint64_t cs = ~(uint64_t)g16(ip + 10) + k.ip_residual + 1;
+        p16(ip + 10, fold_checksum(cs));
+    } else {
+        uint8_t *ip = p + k.ip;
+        if (k.ip + 24 + 16 < k.len && k.ip + 8 + 16 < k.len) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                p32(ip + 24 + 4 * i, k.v6_dst[i]);
+                k.udp_residual += k.v6_dst[i];
+                p32(ip + 8 + 4 * i, k.v6_src[i]);
+                k.udp_residual += k.v6_src[i];
+            }
+        }
+        ip[7] = (uint8_t)k.v6_hop;
+    }
+    uint8_t *udp = p + k.udp;
+    p16(udp + 2, k.udp_dst);
+    p16(udp, k.udp_src);
+    k.udp_residual += k.udp_dst;
+    k.udp_residual += k.udp_src;
+    // path_type is SCION here (the only type process_packet lets through)
+    uint32_t meta = (k.h_meta & 0x00ffffffu) | ((k.curr_hf & 0x3fu) << 24) | (k.curr_inf << 30);
+    p32(p + k.meta, sw32(meta));
+    k.udp_residual += sw32(meta);
+    int inf = k.inf;
+    p16(p + inf + 2, k.seg_id0);
+    k.udp_residual += k.seg_id0;
+    if (k.segment_switch) {
+        inf += 8;
+        if (inf + 8 <= k.len) {
+            k.udp_residual -= g16(p + inf + 2);
+            k.udp_residual += k.seg_id1;
+            p16(p + inf + 2, k.seg_id1);
+        }
+    }
+    uint64_t cs = ~(uint64_t)g16(udp + 6) + k.udp_residual + 1;
+    p16(udp + 6, fold_checksum(cs));
+}
+
+// ---- xdp.c: process_packet -----------------------------------------------------------------
+// Returns the action (> 0 ends the frame), 0 (fall through to the MAC check without a record:
+// the bare `return 0`/ABORT paths) or -1 (rewritten, go to the MAC check).
+template <bool STATS>
+__device__ __forceinline__ int process_packet(BrFrame &k)
+{
+    k.egress_ifindex = -1;
+    int off = parse_underlay(k);
+    if (off < 0) return (int)record<STATS>(k, k.verdict);
+    off = parse_scion(k, off);
+    if (off < 0) return (int)record<STATS>(k, k.verdict);
+
+    uint32_t as_ing_ifid = 0;
+    if (int_iface(k.ifindex) < 0) {
+        int e = ingress_lookup(k);
+        if (e < 0) return (int)record<STATS>(k, V_NO_INTERFACE);
+        as_ing_ifid = s_br.ingress[e].ifid;
+        const uint8_t *hf = k.p + k.hf;
+        uint32_t hf_ing = cons_at(k, k.inf) ? g16(hf + 2) : g16(hf + 4);
+        if (sw16(hf_ing) != as_ing_ifid) return (int)record<STATS>(k, V_NO_INTERFACE);
+    }
+    if (as_ing_ifid != 0)   // path_type == SCION after parse_scion
+        if (!as_ingress(k)) return (int)record<STATS>(k, k.verdict);
+
+    int inf = k.inf;
+    if (k.segment_switch) {
+        inf += 8;
+        if (inf + 8 > k.len) return 0;
+    }
+    const uint8_t *hf = k.p + k.hf;
+    uint32_t key = sw16(cons_at(k, inf) ? g16(hf + 4) : g16(hf + 2));
+    int f = egress_lookup(key);
+    if (f < 0) return (int)record<STATS>(k, V_ABORT);
+    const DevBrEgress &fwd = s_br.egress[f];
+
+    int egress;
+    if (fwd.fwd_external) {
+        if (!as_egress(k, as_ing_ifid)) return (int)record<STATS>(k, k.verdict);
+        if (fwd.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
+        egress = fib_as_egress(k, fwd);
+    } else if (as_ing_ifid != 0) {
+        if (fwd.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
+        egress = fib_egress_br(k, fwd);
+    } else {
+        egress = fib_ip_forward(k);
+    }
+    if (egress < 0) return (int)record<STATS>(k, k.verdict);
+    rewrite(k);
+    k.egress_ifindex = egress;
+    return -1;
+}
+
+__device__ __forceinline__ bool tx_port(int ifindex)
+{
+    if (ifindex < 0 || ifindex >= HFV_BR_MAX_TXPORTS) return false;
+    return (s_br.tx_bits[ifindex >> 5] >> (ifindex & 31)) & 1u;
+}
+
+// ---- kernel ------------------------------------------------------------------------------------
+template <int BLOCK, bool STATS>
+__global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st,
+                                                      const uint32_t *__restrict__ ttab_img, uint8_t *pkts,
+                                                      uint64_t slot, const uint16_t *__restrict__ lens,
+                                                      const uint32_t *__restrict__ ifidx, uint64_t n,
+                                                      uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
+                                                      int32_t *__restrict__ egress,
+                                                      unsigned long long *__restrict__ stats)
+{
+    fill_ttab_dma<2>(ttab_img);
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(&st->br);
+        uint4 *dst = reinterpret_cast<uint4 *>(&s_br);
+        for (uint32_t e = threadIdx.x; e < sizeof(DevBrConfig) / 16; e += BLOCK) dst[e] = src[e];
+    }
+    if constexpr (STATS)
+        for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) s_stats[e] = 0;
+    UniformKey ukey(&st->keys);
+    __syncthreads();
+    const Lane l = lane_bases();
+
+    const uint64_t step = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += step) {
+        BrFrame k = {};
+        k.p = pkts + i * slot;
+        uint32_t len = lens[i];
+        k.len = (int)(len <= slot ? len : slot);
+        k.ifindex = ifidx[i];
+        int a = process_packet<STATS>(k);
+        if (a <= 0) {
+            // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
+            uint32_t v = A_ABORTED;
+            bool ok = true;
+            if (k.need_mac) {
+                uint32_t t0, t1;
+                cmac48_macinput<2>(k.mi, ukey, l, t0, t1);
+                ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
+            }
+            if (!ok) v = V_INVALID_HF;
+            else if (tx_port(k.egress_ifindex)) v = V_FORWARD;
+            a = (int)record<STATS>(k, v);
+        }
+        action[i] = (uint8_t)a;
+        verdict[i] = (uint8_t)k.last_verdict;
+        egress[i] = k.egress_ifindex;
+    }
+    if constexpr (STATS) {
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) {
+            unsigned long long v = s_stats[e];
+            if (v) atomicAdd(stats + e, v);
+        }
+    }
+}
+
+constexpr int kBrBlock = 1024;
+
+int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, const uint16_t *len,
+                      const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
+                      int32_t *egress_ifindex, uint64_t *stats, void *stream, void *ev_start, void *ev_stop)
+{
+    uint64_t blocks = (n + kBrBlock - 1) / kBrBlock;
+    uint64_t cap = (uint64_t)g.num_cus;   // one 1024-thread block per CU (LDS: tables + counters)
+    unsigned grid = (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
+    auto k = stats ? k_br_process<kBrBlock, true> : k_br_process<kBrBlock, false>;
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBrBlock), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, len,
+                          ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
+                          (unsigned long long *)stats);
+    return (int)hipGetLastError();
+}
+
+}  // namespace hfv

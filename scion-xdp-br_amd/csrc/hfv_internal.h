@@ -25,6 +25,53 @@ struct DevKeyTable {
     uint32_t valid[8];
 };
 
+// Router tables as the config-4 kernel sees them (compiled from struct hfv_br_config by
+// hfv_br_set_config).  Addresses/ports keep the BPF code's little-endian view of wire bytes
+// ("l32"/"l16" of the raw field) so they drop straight into the rewrite arithmetic; route
+// prefixes are big-endian words with a precomputed mask for the longest-prefix match.
+struct DevBrIntIface {
+    uint32_t ifindex, family;
+    uint32_t addr[4];   // l32 of addr[4i..4i+3]
+    uint32_t port;      // l16 of port
+};
+struct DevBrIngress {        // ingress_map key {ipv4, ipv6[4], port, u16 ifindex} (common.h:73-84)
+    uint32_t v4, v6[4];      // family INET: v4 = l32(addr), v6 = 0; otherwise v4 = 0, v6 = l32 words
+    uint32_t port;           // l16
+    uint32_t ifindex16;      // ifindex & 0xffff
+    uint32_t ifid;
+};
+struct DevBrEgress {
+    uint32_t ifid, fwd_external, family;
+    uint32_t remote[4], local[4];   // l32 words
+    uint32_t remote_be[4];          // big-endian words of remote (route lookup key)
+    uint32_t remote_port, local_port;   // l16
+};
+struct DevBrRoute {
+    uint32_t family;    // 0: never matches (prefix length beyond the family's width)
+    uint32_t plen;
+    uint32_t pfx[4], mask[4];   // big-endian words, pfx pre-masked
+    int32_t ret;
+    uint32_t ifindex;
+    uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;   // MAC bytes 0-3 / 4-5 as LE words
+};
+struct DevBrConfig {
+    uint32_t n_int, n_ing, n_egr, n_routes;
+    uint32_t tx_bits[HFV_BR_MAX_TXPORTS / 32];
+    DevBrIntIface int_ifaces[HFV_BR_MAX_IFACES];
+    DevBrIngress ingress[HFV_BR_MAX_IFACES];
+    DevBrEgress egress[HFV_BR_MAX_IFACES];
+    DevBrRoute routes[HFV_BR_MAX_ROUTES];
+};
+static_assert(sizeof(DevBrConfig) % 16 == 0, "copied to LDS in 16 B pieces");
+
+// Everything a launch reads from the published device state: the key table (first, so a
+// DevState* is also the DevKeyTable* the verify kernels take) and the router tables.
+struct DevState {
+    DevKeyTable keys;
+    DevBrConfig br;
+};
+void compile_br_config(const hfv_br_config *in, DevBrConfig *out);
+
 enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 
 struct KernelVariant {
@@ -60,6 +107,11 @@ int query_geometry(int device, LaunchGeom *g);
 int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream);
 int build_ttab_image(uint32_t *img, void *stream);
+// full border-router path (hfv_br_kernel.hip)
+int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, const uint16_t *len,
+                      const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
+                      int32_t *egress_ifindex, uint64_t *stats, void *stream, void *ev_start = nullptr,
+                      void *ev_stop = nullptr);
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);

@@ -23,81 +23,12 @@
 
 #include <hip/hip_ext.h>
 
+#include "hfv_aes_dev.h"
 #include "hfv_internal.h"
 
 namespace hfv {
 
-// ---------------------------------------------------------------------------------------
-// tables
-// ---------------------------------------------------------------------------------------
-#define T0V(i) kTables.t0[i]
-#define T0V8(i) T0V(i), T0V(i + 1), T0V(i + 2), T0V(i + 3), T0V(i + 4), T0V(i + 5), T0V(i + 6), T0V(i + 7)
-#define T0V64(i) T0V8(i), T0V8(i + 8), T0V8(i + 16), T0V8(i + 24), T0V8(i + 32), T0V8(i + 40), T0V8(i + 48), T0V8(i + 56)
-__constant__ uint32_t c_t0[256] = {T0V64(0), T0V64(64), T0V64(128), T0V64(192)};
-#undef T0V64
-#undef T0V8
-#undef T0V
-
-// Round tables in LDS.  Layout (byte address of table t at index x for lane L):
-//   (x << 8) | ((t & 1) << 7) | ((L & 31) << 2) | ((t >> 1) << 16)
-// TAB = 2 keeps T0/T1 (64 KiB) and derives T2/T3 by a 16-bit rotation; TAB = 4 stores all
-// four (128 KiB) and needs no rotation.
-__shared__ uint32_t s_tab64[16384];
-__shared__ uint32_t s_tab128[32768];
-__shared__ uint4 s_keys[kDevKeyRows * HFV_MAX_KEYS];   // 48 KiB, round-major
-__shared__ uint32_t s_valid[8];
-__shared__ uint32_t s_next_tile;   // DYN: the block's tile queue head
-
-// v_perm selector for state byte k: address byte 0 <- base byte 0 (copy + T0/T1 bit),
-// byte 1 <- state byte k, byte 2 <- base byte 2 (T2/T3 bit), byte 3 <- 0.
-constexpr uint32_t sel_byte(int k) { return 0x0c020400u | (uint32_t(k) << 8); }
-constexpr uint32_t SEL_B0 = sel_byte(0), SEL_B1 = sel_byte(1), SEL_B2 = sel_byte(2), SEL_B3 = sel_byte(3);
-
-__device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
-
-template <int TAB>
-__device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, uint32_t sel)
-{
-    uint32_t a = __builtin_amdgcn_perm(w, base, sel);
-    if constexpr (TAB == 4)
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab128) + a);
-    else
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab64) + a);
-}
-
-template <int TAB>
-__device__ __forceinline__ void fill_ttab()
-{
-    constexpr int kDwords = TAB == 4 ? 32768 : 16384;
-    uint32_t *dst = TAB == 4 ? s_tab128 : s_tab64;
-#pragma unroll 4
-    for (int e = threadIdx.x; e < kDwords; e += blockDim.x) {
-        uint32_t t = c_t0[(e >> 6) & 255];
-        int rot = 8 * (((e >> 5) & 1) | ((e >> 13) & 2));   // table index * 8
-        dst[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
-    }
-}
-
-// Same table image copied from a prebuilt global copy (ctx->ttab_img, L2-resident after the
-// first blocks) by LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB per wave-instruction
-// straight into LDS, no VGPR round trip and ~16x fewer instructions than fill_ttab.
-template <int TAB>
-__device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
-{
-    constexpr int kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-    for (int c = wave; c < kChunks; c += nw) {
-        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
-    }
-    // vmcnt retires in issue order; the DMA pieces are the youngest loads, and the record
-    // loads issued before them must complete as well before the barrier (the compiler
-    // inserts that wait anyway), so a full drain is the correct and only wait here.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
+// Prebuilt LDS image of the round tables (the fill_ttab_dma source), built once per ctx.
 __global__ void k_build_ttab_image(uint32_t *__restrict__ img)
 {
     int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -106,165 +37,6 @@ __global__ void k_build_ttab_image(uint32_t *__restrict__ img)
     int rot = 8 * (((e >> 5) & 1) | ((e >> 13) & 2));
     img[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
 }
-
-__device__ __forceinline__ void fill_keys(const DevKeyTable *tab)
-{
-    const uint4 *src = reinterpret_cast<const uint4 *>(tab->rows);
-    for (int e = threadIdx.x; e < kDevKeyRows * HFV_MAX_KEYS; e += blockDim.x) s_keys[e] = src[e];
-    if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
-}
-
-// ---------------------------------------------------------------------------------------
-// AES rounds on a column-word state (s[c] = LE u32 of column c)
-// ---------------------------------------------------------------------------------------
-struct Lane {
-    uint32_t b0, b1, b2, b3;   // LDS byte offsets of this lane's copies of T0..T3
-    uint32_t s0, s1, s2, s3;   // v_perm selectors SEL_B0..SEL_B3, held in VGPRs
-    uint32_t f01, f23;         // final-round byte-gather selectors
-};
-
-// Materialise a constant in a VGPR.  v_perm_b32 (VOP3 on gfx9) takes no literal, so its
-// selectors would otherwise occupy SGPRs; the SGPR-resident round keys already bring the
-// kernel close to the 80-SGPR line above which a SIMD holds fewer than 8 waves.
-__device__ __forceinline__ uint32_t vconst(uint32_t c)
-{
-    uint32_t r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(c));
-    return r;
-}
-
-template <int TAB>
-__device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const Lane &l)
-{
-    const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
-    uint32_t n[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b1, l.s1);
-        if constexpr (TAB == 4) {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, l.s2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, l.s3);
-            n[c] = a ^ b ^ x ^ d ^ r[c];
-        } else {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, l.s3);
-            n[c] = a ^ b ^ r[c] ^ rot16(x ^ d);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s[c] = n[c];
-}
-
-// Round 1 for a whitened macinput whose bytes 0,1,8,14,15 are key-only: the five lookups
-// they feed are folded into rk1' (device key row 11, see hfv_tables.h).
-template <int TAB>
-__device__ __forceinline__ void round1_macinput(uint32_t s[4], const uint4 &rk1p, const Lane &l)
-{
-    uint32_t n0, n1, n2, n3;
-    if constexpr (TAB == 4) {
-        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ tlu<TAB>(s[2], l.b2, l.s2) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b3, l.s3) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b2, l.s2) ^ tlu<TAB>(s[1], l.b3, l.s3) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ tlu<TAB>(s[1], l.b2, l.s2) ^ tlu<TAB>(s[2], l.b3, l.s3) ^ rk1p.w;
-    } else {
-        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ rot16(tlu<TAB>(s[2], l.b0, l.s2)) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b1, l.s3)) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b0, l.s2) ^ tlu<TAB>(s[1], l.b1, l.s3)) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ rot16(tlu<TAB>(s[1], l.b0, l.s2) ^ tlu<TAB>(s[2], l.b1, l.s3)) ^ rk1p.w;
-    }
-    s[0] = n0; s[1] = n1; s[2] = n2; s[3] = n3;
-}
-
-// Final round, S(x) taken from byte 1 of T0[x].  All four output columns:
-template <int TAB>
-__device__ __forceinline__ void round_last_full(uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t out[4])
-{
-    const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, l.s1);
-        uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
-        uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, l.s3);
-        out[c] = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ r[c];
-    }
-}
-
-// Final round, only the 48 bits the verifier compares (tag bytes 0..5, xdp.c:89):
-// column 0 whole, column 1 bytes 0-1 (upper half of the result is don't-care).
-template <int TAB>
-__device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t &t0,
-                                              uint32_t &t1)
-{
-    uint32_t a = tlu<TAB>(s[0], l.b0, l.s0), b = tlu<TAB>(s[1], l.b0, l.s1);
-    uint32_t x = tlu<TAB>(s[2], l.b0, l.s2), d = tlu<TAB>(s[3], l.b0, l.s3);
-    t0 = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ rk.x;
-    uint32_t a1 = tlu<TAB>(s[1], l.b0, l.s0), b1 = tlu<TAB>(s[2], l.b0, l.s1);
-    t1 = __builtin_amdgcn_perm(b1, a1, l.f01) ^ rk.y;
-}
-
-// ---------------------------------------------------------------------------------------
-// key sources
-// ---------------------------------------------------------------------------------------
-struct UniformKey {          // slot 0 for every lane, kept in SGPRs
-    uint4 k[kDevKeyRows];
-    bool ok;
-    __device__ __forceinline__ explicit UniformKey(const DevKeyTable *tab)
-    {
-#pragma unroll
-        for (int r = 0; r < kDevKeyRows; ++r) {
-            const uint32_t *p = tab->rows[r][0];
-            k[r] = make_uint4(p[0], p[1], p[2], p[3]);
-        }
-        ok = tab->valid[0] & 1u;
-    }
-    __device__ __forceinline__ uint4 row(int r) const { return k[r]; }
-};
-
-struct LdsKey {              // per-lane slot from the LDS copy of the table
-    uint32_t slot;
-    __device__ __forceinline__ explicit LdsKey(uint32_t s) : slot(s) {}
-    __device__ __forceinline__ uint4 row(int r) const { return s_keys[r * HFV_MAX_KEYS + slot]; }
-    __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
-};
-
-// Tag words 0..1 for a record-derived macinput w[] (bytes 0,1,8,14,15 zero).
-template <int TAB, class K>
-__device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &key, const Lane &l, uint32_t &t0,
-                                                uint32_t &t1)
-{
-    uint4 k0 = key.row(0);
-    uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
-    round1_macinput<TAB>(s, key.row(11), l);
-#pragma unroll
-    for (int r = 2; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
-    round_last_48<TAB>(s, key.row(10), l, t0, t1);
-}
-
-template <int TAB, class K>
-__device__ __forceinline__ void cmac_general(const uint32_t w[4], const K &key, const Lane &l, uint32_t s[4])
-{
-    uint4 k0 = key.row(0);
-    s[0] = w[0] ^ k0.x; s[1] = w[1] ^ k0.y; s[2] = w[2] ^ k0.z; s[3] = w[3] ^ k0.w;
-#pragma unroll
-    for (int r = 1; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
-}
-
-__device__ __forceinline__ Lane lane_bases()
-{
-    uint32_t lane = threadIdx.x & 63;
-    Lane l;
-    l.s0 = vconst(SEL_B0); l.s1 = vconst(SEL_B1); l.s2 = vconst(SEL_B2); l.s3 = vconst(SEL_B3);
-    l.f01 = vconst(0x0c0c0501u); l.f23 = vconst(0x05010c0cu);
-    l.b0 = (lane & 31) << 2;
-    l.b1 = l.b0 | 0x80u;
-    l.b2 = l.b0 | 0x10000u;
-    l.b3 = l.b1 | 0x10000u;
-    return l;
-}
-
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // ---------------------------------------------------------------------------------------
 // record verify: macinput from INF/HF (path_processing.h:39-81), CMAC, 48-bit compare

@@ -72,6 +72,8 @@ def lib():
         "hfv_keymap_erase": (i32, [ctypes.c_char_p, u32]),
         "hfv_keymap_read": (i32, [ctypes.c_char_p, vp, vp]),
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+        "hfv_br_set_config": (i32, [vp, vp]),
+        "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
         "hfv_expand_keys": (i32, [vp, vp, sz, vp, vp]),
@@ -256,6 +258,14 @@ class Ctx:
     def attach_keymap(self, path):
         _check(lib().hfv_ctx_attach_keymap(self._h, path.encode()))
 
+    def br_set_config(self, cfg):
+        _check(lib().hfv_br_set_config(self._h, ctypes.byref(cfg)))
+
+    def br_process(self, pkts, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
+                   stream=None):
+        _check(lib().hfv_br_process(self._h, _ptr(pkts), slot, _ptr(lens), _ptr(ingress_ifindex), n, _ptr(action),
+                                    _ptr(verdict), _ptr(egress_ifindex), _ptr(stats), _stream(stream)))
+
     def verify_macinputs(self, mi, expected, n, pass_bits, key_index=None, stream=None):
         _check(lib().hfv_verify_macinputs(self._h, _ptr(mi), _ptr(expected), _ptr(key_index), n, _ptr(pass_bits),
                                           _stream(stream)))
@@ -272,6 +282,106 @@ class Ctx:
     # host buffers (pinned staging, H2D/kernel/D2H overlapped)
     def verify_records_host(self, recs, n, pass_bits, stride=REC_SIZE):
         _check(lib().hfv_verify_records_host(self._h, _ptr(recs), stride, n, _ptr(pass_bits)))
+
+
+# ---- full BR path (config 4): router tables --------------------------------------------------
+
+AF_INET, AF_INET6 = 2, 10
+BR_MAX_IFACES, BR_MAX_ROUTES, BR_MAX_TXPORTS, BR_COUNTERS, BR_STATS_IFINDEX = 16, 64, 128, 11, 64
+
+
+class BrIntIface(ctypes.Structure):
+    _fields_ = [("ifindex", ctypes.c_uint32), ("family", ctypes.c_uint32), ("addr", ctypes.c_uint8 * 16),
+                ("port", ctypes.c_uint8 * 2), ("pad", ctypes.c_uint8 * 2)]
+
+
+class BrIngress(ctypes.Structure):
+    _fields_ = [("ifindex", ctypes.c_uint32), ("family", ctypes.c_uint32), ("addr", ctypes.c_uint8 * 16),
+                ("port", ctypes.c_uint8 * 2), ("pad", ctypes.c_uint8 * 2), ("ifid", ctypes.c_uint32)]
+
+
+class BrEgress(ctypes.Structure):
+    _fields_ = [("ifid", ctypes.c_uint32), ("fwd_external", ctypes.c_uint32), ("family", ctypes.c_uint32),
+                ("remote", ctypes.c_uint8 * 16), ("local", ctypes.c_uint8 * 16),
+                ("remote_port", ctypes.c_uint8 * 2), ("local_port", ctypes.c_uint8 * 2)]
+
+
+class BrRoute(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_uint32), ("prefix", ctypes.c_uint8 * 16), ("prefix_len", ctypes.c_uint32),
+                ("ret", ctypes.c_int32), ("ifindex", ctypes.c_uint32), ("smac", ctypes.c_uint8 * 6),
+                ("dmac", ctypes.c_uint8 * 6)]
+
+
+class BrConfig(ctypes.Structure):
+    """struct hfv_br_config: the reference's BPF maps (int_iface_map, ingress_map, egress_map,
+    tx_port_map) plus the static next-hop table that replaces bpf_fib_lookup."""
+    _fields_ = [("n_int_ifaces", ctypes.c_uint32), ("n_ingress", ctypes.c_uint32), ("n_egress", ctypes.c_uint32),
+                ("n_routes", ctypes.c_uint32), ("n_tx_ports", ctypes.c_uint32),
+                ("int_ifaces", BrIntIface * BR_MAX_IFACES), ("ingress", BrIngress * BR_MAX_IFACES),
+                ("egress", BrEgress * BR_MAX_IFACES), ("routes", BrRoute * BR_MAX_ROUTES),
+                ("tx_ports", ctypes.c_uint32 * BR_MAX_TXPORTS)]
+
+    @staticmethod
+    def _ip(addr):
+        import ipaddress
+        a = ipaddress.ip_address(addr)
+        b = a.packed + bytes(16 - len(a.packed))
+        return (AF_INET if a.version == 4 else AF_INET6), (ctypes.c_uint8 * 16)(*b)
+
+    @staticmethod
+    def _port(p):
+        return (ctypes.c_uint8 * 2)(p >> 8, p & 0xff)
+
+    @staticmethod
+    def _mac(m):
+        return (ctypes.c_uint8 * 6)(*bytes.fromhex(m.replace(":", "")))
+
+    def add_int_iface(self, ifindex, addr, port):
+        e = self.int_ifaces[self.n_int_ifaces]
+        e.ifindex = ifindex
+        e.family, e.addr = self._ip(addr)
+        e.port = self._port(port)
+        self.n_int_ifaces += 1
+
+    def add_ingress(self, ifindex, addr, port, ifid):
+        e = self.ingress[self.n_ingress]
+        e.ifindex = ifindex
+        e.family, e.addr = self._ip(addr)
+        e.port = self._port(port)
+        e.ifid = ifid
+        self.n_ingress += 1
+
+    def add_egress_link(self, ifid, local, local_port, remote, remote_port):
+        e = self.egress[self.n_egress]
+        e.ifid, e.fwd_external = ifid, 1
+        e.family, e.remote = self._ip(remote)
+        _, e.local = self._ip(local)
+        e.remote_port, e.local_port = self._port(remote_port), self._port(local_port)
+        self.n_egress += 1
+
+    def add_egress_sibling(self, ifid, addr, port):
+        e = self.egress[self.n_egress]
+        e.ifid, e.fwd_external = ifid, 0
+        e.family, e.remote = self._ip(addr)
+        e.remote_port = self._port(port)
+        self.n_egress += 1
+
+    def add_route(self, prefix, prefix_len, ifindex, smac, dmac, ret=0):
+        e = self.routes[self.n_routes]
+        e.family, e.prefix = self._ip(prefix)
+        e.prefix_len, e.ret, e.ifindex = prefix_len, ret, ifindex
+        e.smac, e.dmac = self._mac(smac), self._mac(dmac)
+        self.n_routes += 1
+
+    def add_tx_port(self, ifindex):
+        self.tx_ports[self.n_tx_ports] = ifindex
+        self.n_tx_ports += 1
+
+
+# enum verdict (br/src/bpf/common.h:55-70)
+VERDICT = {"ABORT": 0, "SCION_FORWARD": 12, "PARSE_ERROR": 17, "NOT_SCION": 26, "NOT_IMPLEMENTED": 34,
+           "NO_INTERFACE": 41, "UNDERLAY_MISMATCH": 50, "ROUTER_ALERT": 58, "FIB_LKUP_DROP": 65,
+           "FIB_LKUP_PASS": 74, "INVALID_HF": 81}
 
 
 # ---- pinned key map (bpffs mac_key_map analogue) --------------------------------------------

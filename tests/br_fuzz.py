@@ -1,0 +1,127 @@
+"""Frames for the config-4 parity tests: the PTF scenarios of br/test/ptf_tests/tests.py as
+they enter each BR of the chain, and seeded mutations of them that drive every branch of
+process_packet (parse failures, unknown interfaces, router alerts, bad MACs, segment
+switches, missing routes, ...).  Test infrastructure only.
+"""
+import struct
+
+import numpy as np
+
+import br_topo as T
+from scion_hfv import packets as P
+
+KINDS = ("down", "up", "core", "seg_switch")
+SCENARIOS = (("direct", 1, 2), ("sibling", 1, 3), ("ipfwd", 4, 6))
+
+
+def ptf_cases(v6, mac_fn, seed=0x1234):
+    """[(name, kind, input frame, first BR, ingress ifindex, expected output frame, egress ifindex)]"""
+    out = []
+    for name, ing, egr in SCENARIOS:
+        ing_enc, egr_enc, first, ifi = T.encaps(ing, egr, v6)
+        for kind in KINDS:
+            path = P.ptf_path(kind, ing, egr, T.KEYS, seed=seed, mac_fn=mac_fn)
+            frame = ing_enc.frame(P.scion_header(path.pack()))
+            exp = path.copy().ingress(T.KEYS[1]).egress(T.KEYS[1])
+            want = egr_enc.frame(P.scion_header(exp.pack()))
+            veth_out = {1: 1, 2: 3, 3: 9, 4: 11, 5: 13, 6: 15}[egr]
+            out.append((name, kind, frame, first, ifi, want, veth_out))
+    return out
+
+
+def hop_inputs(brs, v6, mac_fn, seeds=(0x1234, 0xBEEF, 0x0001)):
+    """Every (br, ingress ifindex, frame) a BR sees while the PTF scenarios run through the chain."""
+    res = []
+    for seed in seeds:
+        for name, kind, frame, first, ifi, _, _ in ptf_cases(v6, mac_fn, seed):
+            br, f = first, frame
+            for _ in range(4):
+                res.append((br, ifi, f))
+                buf, lens = T.to_slots([f])
+                a, v, e, s = brs[br].process(buf, lens, np.array([ifi], dtype=np.uint32))
+                f = buf[0, :len(f)].tobytes()
+                if a[0] != 4 or (br, int(e[0])) not in T.LINKS:
+                    break
+                br, ifi = T.LINKS[(br, int(e[0]))]
+    return res
+
+
+IFINDICES = [1, 3, 4, 5, 6, 7, 9, 11, 13, 15, 2, 63, 64, 200]
+
+
+def mutate(rng, frame: bytes, ifindex: int, v6: bool):
+    """One random mutation set; returns (frame bytes, length, ingress ifindex)."""
+    f = bytearray(frame)
+    ip = 14
+    udp = ip + (40 if v6 else 20)
+    sc = udp + 8
+    path = sc + 28 + 8   # host addresses are 4 B + 4 B in these frames
+    inf = path + 4
+    nseg = sum(1 for k in (12, 6, 0) if (struct.unpack_from(">I", f, path)[0] >> k) & 0x3F)
+    hf = inf + 8 * max(nseg, 1)
+    p = rng.random(16)
+    if p[0] < 0.03:
+        f[12:14] = struct.pack(">H", int(rng.choice([0x0806, 0x0800, 0x86DD, 0x8100])))
+    if p[1] < 0.03:
+        f[ip + (6 if v6 else 9)] = int(rng.choice([6, 17, 58]))
+    if p[2] < 0.04 and not v6:
+        f[ip] = 0x40 | int(rng.integers(0, 16))   # IHL: options / invalid
+    if p[3] < 0.05:
+        f[udp + 2:udp + 4] = struct.pack(">H", int(rng.choice([50000, 31002, 1234])))
+    if p[4] < 0.03:
+        f[sc] = int(rng.integers(0, 256))         # version / traffic class
+    if p[5] < 0.05:
+        f[sc + 9] = int(rng.integers(0, 256))     # DT/DL/ST/SL (the 0x2-mask quirk)
+    if p[6] < 0.03:
+        f[sc + 8] = int(rng.choice([0, 1, 2, 3]))  # path type
+    if p[7] < 0.10:                               # path meta: CurrINF/CurrHF/SegLen
+        m = struct.unpack_from(">I", f, path)[0]
+        r = int(rng.integers(0, 4))
+        if r == 0:
+            m ^= 1 << int(rng.integers(24, 32))
+        elif r == 1:
+            m ^= 1 << int(rng.integers(0, 18))
+        else:
+            m = (m & ~(0x3F << 24)) | (int(rng.integers(0, 6)) << 24)
+        struct.pack_into(">I", f, path, m)
+    if p[8] < 0.08:
+        off = inf + 8 * int(rng.integers(0, 2))
+        if off < len(f):
+            f[off] ^= int(rng.choice([1, 2, 0x80]))   # Cons / Peering flags
+    if p[9] < 0.06 and hf < len(f):
+        f[hf] = int(rng.integers(0, 4))           # router alert flags
+    if p[10] < 0.10:                              # MAC / SegID / timestamp / IFID bit flips
+        lo, hi = inf, min(len(f), hf + 36)
+        if hi > lo:
+            b = int(rng.integers(lo, hi))
+            f[b] ^= 1 << int(rng.integers(0, 8))
+    if p[11] < 0.04:
+        f[ip + (7 if v6 else 8)] = int(rng.integers(0, 256))   # TTL / hop limit
+    n = len(f)
+    if p[12] < 0.08:
+        n = int(rng.integers(0, len(f) + 1))      # truncated frame
+    if p[13] < 0.08:
+        ifindex = int(rng.choice(IFINDICES))
+    return bytes(f), n, ifindex
+
+
+def fuzz_batch(hops, br, v6, n, seed, slot=T.SLOT, payload_max=0):
+    """n frames for BR `br`: hop inputs of that BR (and a few of other BRs), mutated.
+    payload_max > 0 pads frames with random payload up to that many bytes (mixed sizes)."""
+    rng = np.random.default_rng(seed)
+    mine = [h for h in hops if h[0] == br] or hops
+    frames = np.zeros((n, slot), dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint16)
+    ifidx = np.zeros(n, dtype=np.uint32)
+    for i in range(n):
+        src = mine if rng.random() < 0.9 else hops
+        _, ifi, f = src[int(rng.integers(0, len(src)))]
+        f, ln, ifi = mutate(rng, f, ifi, v6)
+        if payload_max and ln == len(f):
+            extra = int(rng.integers(0, max(1, min(payload_max, slot) - len(f))))
+            f = f + rng.integers(0, 256, extra, dtype=np.uint8).tobytes()
+            ln = len(f)
+        frames[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+        lens[i] = ln
+        ifidx[i] = ifi
+    return frames, lens, ifidx

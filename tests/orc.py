@@ -141,5 +141,26 @@ def expected_pass_rule(n, seed=SEED_RECORDS, first_index=0):
     return (z & np.uint64(15)) != 0
 
 
+BR_STATS_SHAPE = (64, 2, 11)   # HFV_BR_STATS_IFINDEX x (bytes, packets) x HFV_BR_COUNTERS
+
+
+def br_process(frames, lens, ifidx, cfg, key0_hop_key=None, stats=None):
+    """Oracle border router (hfv_br_oracle.c) over frames[n, slot] in place.
+    Returns (action u8[n], verdict u8[n], egress i32[n], stats u64[64, 2, 11])."""
+    n, slot = frames.shape
+    assert frames.dtype == np.uint8 and frames.flags.c_contiguous
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    ifidx = np.ascontiguousarray(ifidx, dtype=np.uint32)
+    action = np.zeros(n, dtype=np.uint8)
+    verdict = np.zeros(n, dtype=np.uint8)
+    egress = np.zeros(n, dtype=np.int32)
+    if stats is None:
+        stats = np.zeros(BR_STATS_SHAPE, dtype=np.uint64)
+    key = ctypes.create_string_buffer(bytes(key0_hop_key), 192) if key0_hop_key is not None else None
+    oracle().orc_br_process(_vp(frames), ctypes.c_size_t(slot), _vp(lens), _vp(ifidx), ctypes.c_size_t(n),
+                            ctypes.byref(cfg), key, _vp(action), _vp(verdict), _vp(egress), _vp(stats))
+    return action, verdict, egress, stats
+
+
 def load_golden(name):
     return dict(np.load(os.path.join(GOLDEN, name)))

@@ -1,0 +1,100 @@
+"""Config 4 on the GPU: hfv_br_process (hfv_br_kernel.hip) against the oracle border router,
+bit-exact on frames (every byte of every slot), XDP action, verdict, redirect target and the
+verdict counters; plus the PTF scenarios end to end through chained GPU routers."""
+import numpy as np
+import pytest
+
+import br_fuzz as F
+import br_topo as T
+import orc
+import scion_hfv as hfv
+
+pytestmark = pytest.mark.gpu
+MAC = lambda k, m: orc.cmac(m, k)   # noqa: E731
+
+
+def _gpu_brs(ctx, v6, key0=T.KEYS[1]):
+    return {b: T.GpuBR(ctx, T.br_config(b, v6), key0=key0) for b in ("br1", "br2", "br3")}
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+def test_ptf_scenarios_gpu(gpu_ctx, v6):
+    brs = _gpu_brs(gpu_ctx, v6)
+    for name, kind, frame, first, ifi, want, veth_out in F.ptf_cases(v6, MAC):
+        out, last, egress, trace = T.run_chain(brs, frame, first, ifi)
+        assert out == want, (name, kind)
+        assert egress == veth_out
+        for br, a, v, _ in trace:
+            assert (a, v) == (4, hfv.VERDICT["SCION_FORWARD"])
+        s = trace[0][3]
+        assert s[ifi, 0, 1] == len(frame) and s[ifi, 1, 1] == 1 and s.sum() == len(frame) + 1
+
+
+def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0):
+    ref = frames.copy()
+    oa, ov, oe, os_ = orc.br_process(ref, lens, ifidx, cfg, orc.hop_key(key0) if key0 is not None else None)
+    got = frames.copy()
+    ga, gv, ge, gs = T.GpuBR(gpu_ctx, cfg, key0=key0).process(got, lens, ifidx)
+    bad = np.nonzero((ga != oa) | (gv != ov) | (ge != oe) | (got != ref).any(axis=1))[0]
+    assert bad.size == 0, "first mismatch at frame %d: gpu (%d,%d,%d) oracle (%d,%d,%d)" % (
+        bad[0], ga[bad[0]], gv[bad[0]], ge[bad[0]], oa[bad[0]], ov[bad[0]], oe[bad[0]])
+    assert (gs == os_).all()
+    return ov
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+@pytest.mark.parametrize("br", ["br1", "br2", "br3"])
+def test_fuzz_parity(gpu_ctx, br, v6):
+    brs = {b: T.OracleBR(T.br_config(b, v6)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, v6, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, br, v6, 20000, seed=100 + v6, payload_max=1500)
+    verdicts = _compare(gpu_ctx, frames, lens, ifidx, T.br_config(br, v6), T.KEYS[1])
+    assert len(np.unique(verdicts)) >= 6
+
+
+def test_fuzz_parity_no_key_and_foreign_key(gpu_ctx):
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 4000, seed=7)
+    v = _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), None)
+    assert hfv.VERDICT["SCION_FORWARD"] not in v
+    _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[5])
+
+
+def test_large_batch_mixed_sizes(gpu_ctx):
+    """2^17 frames of 64..1500 B in 2 KiB slots (the config-4 shape): parity with the oracle."""
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 1 << 17, seed=3, payload_max=1500)
+    _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[1])
+
+
+def test_stats_accumulate_and_bad_args(gpu_ctx):
+    import torch
+    ing_enc, egr_enc, first, ifi = T.encaps(1, 2, False)
+    from scion_hfv import packets as P
+    frame = ing_enc.frame(P.scion_header(P.ptf_path("down", 1, 2, T.KEYS, seed=9, mac_fn=MAC).pack()))
+    buf, lens = T.to_slots([frame] * 100)
+    gpu_ctx.br_set_config(T.br_config("br1"))
+    gpu_ctx.key_add(0, T.KEYS[1])
+    d = torch.from_numpy(buf).cuda()
+    dl = torch.from_numpy(lens.view(np.int16)).cuda()
+    di = torch.full((100,), ifi, dtype=torch.int32, device="cuda")
+    a = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    v = torch.zeros_like(a)
+    e = torch.zeros(100, dtype=torch.int32, device="cuda")
+    s = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
+    gpu_ctx.br_process(d, T.SLOT, dl, di, 100, a, v, e, s)
+    gpu_ctx.br_process(d, T.SLOT, dl, di, 100, a, v, e, s)   # second pass: now addressed to the next AS
+    torch.cuda.synchronize()
+    st = s.cpu().numpy().reshape(64, 2, 11)
+    assert st[ifi, 1, 1] == 100 and st[ifi, 1, 5] == 100          # FORWARD, then NO_INTERFACE
+    assert st[ifi, 0, 1] == 100 * len(frame)
+    with pytest.raises(hfv.HfvError):
+        gpu_ctx.br_process(d, 60, dl, di, 100, a, v, e, s)       # slot < 64
+    with pytest.raises(hfv.HfvError):
+        gpu_ctx.br_process(d, 2044, dl, di, 100, a, v, e, s)     # slot % 8
+    cfg = T.br_config("br1")
+    cfg.n_routes = 65
+    with pytest.raises(hfv.HfvError):
+        gpu_ctx.br_set_config(cfg)

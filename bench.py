@@ -18,6 +18,14 @@ prints one JSON line.  Besides the contract fields it carries:
                    verdicts cross-checked against the GPU bitmap.
   hbm_resident  -- the same kernel on 2^24 records (1 GiB > 256 MiB Infinity Cache).
   host_e2e      -- rate including H2D/D2H through pinned staging (hfv_verify_records_host).
+
+    python bench.py --workload br [--n 1048576] [--steps 10]
+
+runs config 4 instead: the full border-router per-packet path (hfv_br_process: parse,
+AS ingress/egress, next hop, rewrite, MAC check, counters) as BR 1 of the reference test
+topology, over n frames of 64..1500 B in 2 KiB slots (PTF scenario traffic, 1/16 with a
+corrupted hop-field MAC).  Frames are rewritten in place, so each timed step gets its own
+pristine copy of the batch (K copies resident in HBM, made before the timed region).
 """
 import argparse
 import json
@@ -142,6 +150,163 @@ def cpu_baseline(recs_host, keysel, gpu_bits, budget_s):
     return out
 
 
+BR_SLOT = 2048
+BR_KINDS = ("down", "up", "core", "seg_switch")
+
+
+def br_templates():
+    """Frames BR 1 of the reference topology receives in the PTF scenarios (as ingress from
+    AS interfaces 1/2, and from sibling BR 2 over the internal link), each also with a
+    corrupted hop-field MAC.  Returns (frames, ifindex, good, algorithmic bytes) lists."""
+    from scion_hfv import packets as P
+    from scion_hfv import topology as TP
+    frames, ifis, good, abytes = [], [], [], []
+    for ki, kind in enumerate(BR_KINDS):
+        flows = [((1, 2), None), ((2, 1), None), ((1, 3), None), ((2, 4), None), ((3, 1), 5), ((4, 2), 5)]
+        for fi, ((ing, egr), internal) in enumerate(flows):
+            path = P.ptf_path(kind, ing, egr, TP.KEYS, seed=0x100 * ki + fi)
+            if internal:   # BR 2 did the AS ingress and handed the frame over veth4 -> veth5
+                path.ingress(TP.KEYS[1])
+                enc, ifi = P.Encap(TP.MAC[4], TP.MAC[5], "10.2.0.0", "10.2.0.1", 31002, 31002), internal
+            else:
+                enc, _, _, ifi = TP.encaps(ing, egr)
+            switch = kind == "seg_switch" and not internal
+            for bad in (False, True):
+                p = path.copy()
+                if bad:
+                    h = p.hops[p.curr_hf]
+                    h.mac = bytes([h.mac[0] ^ 0x10]) + h.mac[1:]
+                f = enc.frame(P.scion_header(p.pack()))
+                # header bytes through the last hop field read, + bytes rewritten (Ethernet 12,
+                # IPv4 11, UDP 6, PathMeta 4, SegID 2 per info field touched) + 12 B of per-frame
+                # metadata (len, ifindex in; action, verdict, egress out)
+                hf_end = 78 + 4 + 8 * len(p.infos) + 12 * (p.curr_hf + 1 + switch)
+                frames.append(f)
+                ifis.append(ifi)
+                good.append(not bad)
+                abytes.append(hf_end + 35 + 2 * (1 + switch) + 12)
+    return frames, ifis, good, abytes
+
+
+def corrupted(n, first_index=0):
+    """Same 1/16 corruption draw as the 64 B records (splitmix64 draw 4i+2 & 15 == 0)."""
+    i = np.arange(first_index, first_index + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(SEED_RECORDS) + (np.uint64(4) * i + np.uint64(3)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(15)) == 0
+
+
+def br_cpu_baseline(frames_host, lens, ifidx, cfg, budget_s):
+    """The oracle border router (a scalar C restatement of xdp.c; the BPF program itself cannot
+    run here) on one host core over a sample of the same frames."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc   # test infrastructure: only the cpu_baseline leg may use it
+    from scion_hfv import topology as TP
+    hk = orc.hop_key(TP.KEYS[1])
+    reps, t_all, n = 0, 0.0, len(frames_host)
+    while t_all < budget_s or reps == 0:
+        work = frames_host.copy()
+        t0 = time.perf_counter()
+        a, v, e, s = orc.br_process(work, lens, ifidx, cfg, hk)
+        t_all += time.perf_counter() - t0
+        reps += 1
+    return a, {"value": round(n * reps / t_all / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+               "sample": f"{n} frames of the benched mix x {reps} passes, oracle/hfv_br_oracle.c (scalar restatement "
+                         f"of br/src/bpf/xdp.c process_packet + verify), 1 thread"}
+
+
+def run_br(args, rank, world, local):
+    from scion_hfv import topology as TP
+    n, steps = args.n, args.steps
+    if steps > 32:
+        raise SystemExit("--workload br keeps one pristine 2 KiB-slot batch per timed step in HBM: use --steps <= 32")
+    ctx = hfv.Ctx(local)
+    ctx.key_add(0, TP.KEYS[1])
+    cfg = TP.br_config("br1")
+    ctx.br_set_config(cfg)
+    stream = torch.cuda.current_stream().cuda_stream
+    frames, ifis, good, abytes = br_templates()
+    nt = len(frames) // 2
+    rng = np.random.default_rng(0x5C100004 + rank)
+    tid = (np.arange(n) % nt) * 2 + corrupted(n, rank * n)          # template = 2 * flow + bad
+    hdr = np.array([len(f) for f in frames])
+    lens = np.maximum(hdr[tid], rng.integers(64, 1501, n)).astype(np.uint16)
+    tmpl = np.zeros((len(frames), BR_SLOT), dtype=np.uint8)
+    for i, f in enumerate(frames):
+        tmpl[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+    d_tid = torch.from_numpy(tid.astype(np.int64)).cuda()
+    master = torch.from_numpy(tmpl).cuda()[d_tid]                    # n x 2 KiB, gathered on device
+    d_len = torch.from_numpy(lens.view(np.int16)).cuda()
+    d_if = torch.from_numpy(np.array(ifis, dtype=np.int32)).cuda()[d_tid]
+    act = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    ver = torch.zeros_like(act)
+    egr = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
+    n_good = int(np.array(good)[tid].sum())
+    alg = float(np.array(abytes)[tid].mean())
+
+    work = torch.empty_like(master)
+    for _ in range(max(1, args.warmup)):
+        work.copy_(master)
+        ctx.br_process(work, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream)
+    torch.cuda.synchronize()
+    assert int((act == 4).sum()) == n_good and int((ver == hfv.VERDICT["INVALID_HF"]).sum()) == n - n_good
+    del work
+    copies = [master.clone() for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in copies:
+        ctx.br_process(c, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ks = []
+    for c in copies[: min(steps, 10)]:
+        c.copy_(master)
+        ks.append(ctx.br_process_timed(c, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream))
+    ks.sort()
+    k_mean = float(np.mean(ks))
+    achieved = alg * n / (k_mean * 1e-3) / 1e9
+    result = {
+        "metric": "Mpkt/s full border-router per-packet path (parse + hop-field MAC verify + rewrite), "
+                  "mixed 64-1500 B frames",
+        "value": round(world * n * steps / elapsed / 1e6, 2),
+        "unit": "Mpkt/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (PTF scenario frames of the reference test topology for BR 1, 24 flows, 64-1500 B, "
+                "2 KiB slots, 1/16 corrupted MACs)",
+        "config": {"workload": f"config 4: {n} frames per GPU through hfv_br_process as br1-ff00_0_1-1",
+                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "parallelism": f"batch-sharded x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_br_process",
+                     "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(ks[len(ks) // 2], 5),
+                     "algorithmic_bytes_per_frame": round(alg, 2),
+                     "kernel_mpkts": round(n / k_mean / 1e3, 1)},
+    }
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        m = min(n, 1 << 16)
+        hf = master[:m].cpu().numpy()
+        a_cpu, result["cpu_baseline"] = br_cpu_baseline(hf, lens[:m], np.array(ifis, dtype=np.uint32)[tid[:m]],
+                                                        cfg, min(args.cpu_budget, 5.0))
+        result["cpu_baseline"]["actions_match_gpu"] = bool((a_cpu == act[:m].cpu().numpy()).all())
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +317,8 @@ def main():
     ap.add_argument("--big-n", type=int, default=1 << 24, help="HBM-resident run size (0 = skip)")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
     ap.add_argument("--no-host-e2e", action="store_true")
+    ap.add_argument("--workload", choices=["hf", "br"], default="hf",
+                    help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,6 +327,8 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.workload == "br":
+        return run_br(args, rank, world, local)
     keysel = hfv.KEYSEL_IFID if args.keysel == "ifid" else hfv.KEYSEL_ZERO
     n = args.n
 

@@ -225,6 +225,11 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
 int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex,
                    size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats,
                    void *stream);
+/* Same, then waits for the launch and returns its execution time (start/stop of the kernel
+ * dispatch itself) in *kernel_ms.  For benchmarks. */
+int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len,
+                         const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
+                         int32_t *egress_ifindex, uint64_t *stats, void *stream, float *kernel_ms);
 
 /* ---- host helpers ---------------------------------------------------------------------- */
 /* Scalar verify_hop_field on the host (SURVEY.md 8b v) for control-plane checks. */

@@ -628,6 +628,32 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
     return after_launch(ctx, st, e, "br_process launch");
 }
 
+int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len,
+                         const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
+                         int32_t *egress_ifindex, uint64_t *stats, void *stream, float *kernel_ms)
+{
+    if (!kernel_ms) return fail(-EINVAL, "kernel_ms is NULL");
+    *kernel_ms = 0.0f;
+    if (n == 0) return ctx ? 0 : fail(-EINVAL, "ctx is NULL");
+    int rc = br_args(ctx, pkts, slot, len, ingress_ifindex, action, verdict, egress_ifindex);
+    if (rc) return rc;
+    if ((uintptr_t)stats & 7) return fail(-EINVAL, "misaligned stats");
+    DeviceGuard g(ctx->device);
+    for (int i = 0; i < 2; ++i)
+        if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
+    hipStream_t st = pick_stream(ctx, stream);
+    DevState *ds;
+    rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_br_process(ctx->geom, ds, pkts, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex,
+                              stats, st, ctx->tev[0], ctx->tev[1]);
+    rc = after_launch(ctx, st, e, "br_process launch");
+    if (rc) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->tev[1]));
+    HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
 // streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.
 int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits)

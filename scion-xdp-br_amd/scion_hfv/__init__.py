@@ -74,6 +74,7 @@ def lib():
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
         "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
+        "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
         "hfv_expand_keys": (i32, [vp, vp, sz, vp, vp]),
@@ -265,6 +266,14 @@ class Ctx:
                    stream=None):
         _check(lib().hfv_br_process(self._h, _ptr(pkts), slot, _ptr(lens), _ptr(ingress_ifindex), n, _ptr(action),
                                     _ptr(verdict), _ptr(egress_ifindex), _ptr(stats), _stream(stream)))
+
+    def br_process_timed(self, pkts, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
+                         stream=None):
+        ms = ctypes.c_float(0.0)
+        _check(lib().hfv_br_process_timed(self._h, _ptr(pkts), slot, _ptr(lens), _ptr(ingress_ifindex), n,
+                                          _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats),
+                                          _stream(stream), ctypes.byref(ms)))
+        return ms.value
 
     def verify_macinputs(self, mi, expected, n, pass_bits, key_index=None, stream=None):
         _check(lib().hfv_verify_macinputs(self._h, _ptr(mi), _ptr(expected), _ptr(key_index), n, _ptr(pass_bits),

@@ -27,9 +27,16 @@ fi
 if [[ $MODE == all || $MODE == bench ]]; then
     step bench 600 python bench.py || exit $?
 fi
+if [[ $MODE == all || $MODE == bench || $MODE == br ]]; then
+    step bench_br 600 python bench.py --workload br || exit $?
+fi
 if [[ $MODE == all || $MODE == prof ]]; then
     # the same command as the bench step, under the kernel tracer
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
         python3 bench.py || exit $?
     python3 scripts/prof_summary.py $OUT/prof/run_kernel_trace.csv $OUT/prof/verify_by_batch.json
+fi
+if [[ $MODE == all || $MODE == prof || $MODE == br ]]; then
+    step rocprof_br 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_br -o run -- \
+        python3 bench.py --workload br --cpu-budget 0 || exit $?
 fi

@@ -105,6 +105,14 @@ __device__ __forceinline__ uint32_t vconst(uint32_t c)
     return r;
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32 (gfx950)
+}
+
+// One full round.  TAB = 2 expects the round key pre-rotated by 16 (device key image rows
+// 1..9) and folds it into the rotated half: 2 x xor3 + 1 rotate per column; TAB = 4 expects
+// the plain round key: 2 x xor3 per column.
 template <int TAB>
 __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const Lane &l)
 {
@@ -117,11 +125,11 @@ __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const
         if constexpr (TAB == 4) {
             uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, l.s2);
             uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, l.s3);
-            n[c] = a ^ b ^ x ^ d ^ r[c];
+            n[c] = xor3(xor3(a, b, x), d, r[c]);
         } else {
             uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
             uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, l.s3);
-            n[c] = a ^ b ^ r[c] ^ rot16(x ^ d);
+            n[c] = xor3(a, b, rot16(xor3(x, d, r[c])));
         }
     }
 #pragma unroll
@@ -135,15 +143,15 @@ __device__ __forceinline__ void round1_macinput(uint32_t s[4], const uint4 &rk1p
 {
     uint32_t n0, n1, n2, n3;
     if constexpr (TAB == 4) {
-        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ tlu<TAB>(s[2], l.b2, l.s2) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b3, l.s3) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ tlu<TAB>(s[0], l.b2, l.s2) ^ tlu<TAB>(s[1], l.b3, l.s3) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ tlu<TAB>(s[1], l.b2, l.s2) ^ tlu<TAB>(s[2], l.b3, l.s3) ^ rk1p.w;
+        n0 = xor3(tlu<TAB>(s[1], l.b1, l.s1), tlu<TAB>(s[2], l.b2, l.s2), rk1p.x);
+        n1 = xor3(xor3(tlu<TAB>(s[1], l.b0, l.s0), tlu<TAB>(s[2], l.b1, l.s1), tlu<TAB>(s[0], l.b3, l.s3)), rk1p.y, 0u);
+        n2 = xor3(xor3(tlu<TAB>(s[3], l.b1, l.s1), tlu<TAB>(s[0], l.b2, l.s2), tlu<TAB>(s[1], l.b3, l.s3)), rk1p.z, 0u);
+        n3 = xor3(xor3(tlu<TAB>(s[3], l.b0, l.s0), tlu<TAB>(s[1], l.b2, l.s2), tlu<TAB>(s[2], l.b3, l.s3)), rk1p.w, 0u);
     } else {
-        n0 = tlu<TAB>(s[1], l.b1, l.s1) ^ rot16(tlu<TAB>(s[2], l.b0, l.s2)) ^ rk1p.x;
-        n1 = tlu<TAB>(s[1], l.b0, l.s0) ^ tlu<TAB>(s[2], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b1, l.s3)) ^ rk1p.y;
-        n2 = tlu<TAB>(s[3], l.b1, l.s1) ^ rot16(tlu<TAB>(s[0], l.b0, l.s2) ^ tlu<TAB>(s[1], l.b1, l.s3)) ^ rk1p.z;
-        n3 = tlu<TAB>(s[3], l.b0, l.s0) ^ rot16(tlu<TAB>(s[1], l.b0, l.s2) ^ tlu<TAB>(s[2], l.b1, l.s3)) ^ rk1p.w;
+        n0 = xor3(tlu<TAB>(s[1], l.b1, l.s1), rot16(tlu<TAB>(s[2], l.b0, l.s2)), rk1p.x);
+        n1 = xor3(tlu<TAB>(s[1], l.b0, l.s0), tlu<TAB>(s[2], l.b1, l.s1), rk1p.y) ^ rot16(tlu<TAB>(s[0], l.b1, l.s3));
+        n2 = xor3(tlu<TAB>(s[3], l.b1, l.s1), rot16(tlu<TAB>(s[0], l.b0, l.s2) ^ tlu<TAB>(s[1], l.b1, l.s3)), rk1p.z);
+        n3 = xor3(tlu<TAB>(s[3], l.b0, l.s0), rot16(tlu<TAB>(s[1], l.b0, l.s2) ^ tlu<TAB>(s[2], l.b1, l.s3)), rk1p.w);
     }
     s[0] = n0; s[1] = n1; s[2] = n2; s[3] = n3;
 }
@@ -159,7 +167,7 @@ __device__ __forceinline__ void round_last_full(uint32_t s[4], const uint4 &rk, 
         uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, l.s1);
         uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
         uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, l.s3);
-        out[c] = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ r[c];
+        out[c] = xor3(__builtin_amdgcn_perm(b, a, l.f01), __builtin_amdgcn_perm(d, x, l.f23), r[c]);
     }
 }
 
@@ -171,7 +179,7 @@ __device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &
 {
     uint32_t a = tlu<TAB>(s[0], l.b0, l.s0), b = tlu<TAB>(s[1], l.b0, l.s1);
     uint32_t x = tlu<TAB>(s[2], l.b0, l.s2), d = tlu<TAB>(s[3], l.b0, l.s3);
-    t0 = __builtin_amdgcn_perm(b, a, l.f01) ^ __builtin_amdgcn_perm(d, x, l.f23) ^ rk.x;
+    t0 = xor3(__builtin_amdgcn_perm(b, a, l.f01), __builtin_amdgcn_perm(d, x, l.f23), rk.x);
     uint32_t a1 = tlu<TAB>(s[1], l.b0, l.s0), b1 = tlu<TAB>(s[2], l.b0, l.s1);
     t1 = __builtin_amdgcn_perm(b1, a1, l.f01) ^ rk.y;
 }
@@ -179,6 +187,8 @@ __device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &
 // ---------------------------------------------------------------------------------------
 // key sources
 // ---------------------------------------------------------------------------------------
+// Key sources.  row(r) is the device key image row as stored (hfv_tables.h); rk<TAB>(r) is
+// the form round_full<TAB> takes for rounds 1..9 (image rows are pre-rotated for TAB = 2).
 struct UniformKey {          // slot 0 for every lane, kept in SGPRs
     uint4 k[kDevKeyRows];
     bool ok;
@@ -192,12 +202,28 @@ struct UniformKey {          // slot 0 for every lane, kept in SGPRs
         ok = tab->valid[0] & 1u;
     }
     __device__ __forceinline__ uint4 row(int r) const { return k[r]; }
+    template <int TAB>
+    __device__ __forceinline__ uint4 rk(int r) const
+    {
+        if constexpr (TAB == 2) {
+            return k[r];
+        } else {   // undo the image's rotation; uniform operands, so these stay scalar
+            auto u = [](uint32_t x) { return (x >> 16) | (x << 16); };
+            return make_uint4(u(k[r].x), u(k[r].y), u(k[r].z), u(k[r].w));
+        }
+    }
 };
 
 struct LdsKey {              // per-lane slot from the LDS copy of the table
     uint32_t slot;
     __device__ __forceinline__ explicit LdsKey(uint32_t s) : slot(s) {}
     __device__ __forceinline__ uint4 row(int r) const { return s_keys[r * HFV_MAX_KEYS + slot]; }
+    template <int TAB>
+    __device__ __forceinline__ uint4 rk(int r) const
+    {
+        static_assert(TAB == 2, "per-lane keys use the 64 KiB two-table layout");
+        return row(r);
+    }
     __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
 };
 
@@ -210,7 +236,7 @@ __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &ke
     uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
     round1_macinput<TAB>(s, key.row(11), l);
 #pragma unroll
-    for (int r = 2; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
+    for (int r = 2; r < 10; ++r) round_full<TAB>(s, key.template rk<TAB>(r), l);
     round_last_48<TAB>(s, key.row(10), l, t0, t1);
 }
 
@@ -220,7 +246,7 @@ __device__ __forceinline__ void cmac_general(const uint32_t w[4], const K &key, 
     uint4 k0 = key.row(0);
     s[0] = w[0] ^ k0.x; s[1] = w[1] ^ k0.y; s[2] = w[2] ^ k0.z; s[3] = w[3] ^ k0.w;
 #pragma unroll
-    for (int r = 1; r < 10; ++r) round_full<TAB>(s, key.row(r), l);
+    for (int r = 1; r < 10; ++r) round_full<TAB>(s, key.template rk<TAB>(r), l);
 }
 
 __device__ __forceinline__ Lane lane_bases()

@@ -97,6 +97,7 @@ void compile_dev_key(const hop_key *hk, uint32_t dk[4 * kDevKeyRows])
     dk[45] = rk[5] ^ T(2, k[3] >> 16);                          // col 1: row2 <- byte 14
     dk[46] = rk[6] ^ T(0, k[2]);                                // col 2: row0 <- byte 8
     dk[47] = rk[7] ^ T(1, k[0] >> 8);                           // col 3: row1 <- byte 1
+    for (int i = 4; i < 40; ++i) dk[i] = rotl32(dk[i], 16);    // rows 1..9 pre-rotated (hfv_tables.h)
 }
 
 }  // namespace hfv

@@ -118,8 +118,8 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
     for (int r = 2; r < 10; ++r) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-            if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round_full<TAB>(s[p], ukey->row(r), l);
-            else round_full<TAB>(s[p], LdsKey(slot[p]).row(r), l);
+            if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round_full<TAB>(s[p], ukey->template rk<TAB>(r), l);
+            else round_full<TAB>(s[p], LdsKey(slot[p]).template rk<TAB>(r), l);
         }
     }
 #pragma unroll
@@ -405,9 +405,10 @@ __global__ __launch_bounds__(256) void k_expand_keys(const uint4 *__restrict__ r
         uint32_t k0[4] = {w[0] ^ k1[0], w[1] ^ k1[1], w[2] ^ k1[2], w[3] ^ k1[3]};
         uint32_t *row0 = tab->rows[0][slot];
         row0[0] = k0[0]; row0[1] = k0[1]; row0[2] = k0[2]; row0[3] = k0[3];
-        for (int r = 1; r < 11; ++r) {
+        for (int r = 1; r < 11; ++r) {   // rows 1..9 pre-rotated by 16 (hfv_tables.h)
             uint32_t *p = tab->rows[r][slot];
-            p[0] = w[4 * r]; p[1] = w[4 * r + 1]; p[2] = w[4 * r + 2]; p[3] = w[4 * r + 3];
+            int rot = r < 10 ? 16 : 0;
+            for (int c = 0; c < 4; ++c) p[c] = rot ? __builtin_amdgcn_alignbit(w[4 * r + c], w[4 * r + c], 16) : w[4 * r + c];
         }
         uint32_t *p = tab->rows[11][slot];
         p[0] = w[4] ^ tg(0, k0[0]) ^ tg(3, k0[3] >> 24);

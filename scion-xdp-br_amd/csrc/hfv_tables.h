@@ -52,11 +52,14 @@ static_assert(kTables.sbox[0x00] == 0x63 && kTables.sbox[0x01] == 0x7c && kTable
                   kTables.sbox[0xff] == 0x16,
               "S-box generation (FIPS-197 Figure 7 spot values)");
 
-constexpr uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
+constexpr uint32_t rotl32(uint32_t x, int s) { return s & 31 ? (x << (s & 31)) | (x >> (32 - (s & 31))) : x; }
 
 // Device key image consumed by the kernels (192 B = 12 x 16 B), compiled from a hop_key:
 //   row 0      k0x   = rk0 ^ K1          (CMAC whitening folded into round 0)
-//   rows 1..10 rk1 .. rk10
+//   rows 1..9  rot16(rk1) .. rot16(rk9)  (the two-table round adds its key inside the
+//                      16-bit-rotated half: n = T0 ^ T1 ^ rot16(T0' ^ T1' ^ rot16(rk)),
+//                      two 3-input XORs and one rotate per column)
+//   row 10     rk10  (final round)
 //   row 11     rk1'  = rk1 ^ the five round-1 table terms whose inputs are the constant-zero
 //                      macinput bytes 0,1,8,14,15 (scion.h:122-132), i.e. key-only values.
 // Row 11 is only valid for inputs with those bytes zero (records built by the verifier).

@@ -1,0 +1,186 @@
+"""Control-plane tables: br-loader's TOML + topology.json path
+(br/src/config.cpp, maps.cpp) rebuilt by scion_hfv.config, and the verdict-counter view of
+`br-loader watch` (br/src/stats.cpp) in scion_hfv.stats.
+
+The TOML/JSON inputs are written by the test in the format of br/test/br_config/ for the
+three-router topology of scion_hfv.topology; the tables the loader builds must drive the
+oracle router through the PTF scenarios exactly like the hand-built ones."""
+import ctypes
+import io
+import json
+
+import numpy as np
+import pytest
+
+import br_fuzz as F
+import br_topo as T
+import orc
+import scion_hfv as hfv
+from scion_hfv import config as C
+from scion_hfv import stats as S
+from scion_hfv import topology as TP
+
+MAC = lambda k, m: orc.cmac(m, k)   # noqa: E731
+BRS = {"br1": "br1-ff00_0_1-1", "br2": "br1-ff00_0_1-2", "br3": "br1-ff00_0_1-3"}
+
+
+def _fmt(ip, port):
+    return ("[%s]:%d" if ":" in ip else "%s:%d") % (ip, port)
+
+
+def write_topology(tmp_path, v6):
+    ext, internal = TP._addrs(v6)
+    topo = {"border_routers": {}}
+    for short, full in BRS.items():
+        ifaces = {}
+        for ifid, veth, rveth in TP._BRS[short]["ext"]:
+            ifaces[str(ifid)] = {"underlay": {"public": _fmt(ext(ifid, 2), 50000), "remote": _fmt(ext(ifid, 1), 50000)},
+                                 "isd_as": "1-ff00:0:%d" % (ifid + 1), "link_to": "CHILD", "mtu": 1472}
+        topo["border_routers"][full] = {"internal_addr": _fmt(internal[short][0], 31002), "interfaces": ifaces}
+    tp = tmp_path / ("topology6.json" if v6 else "topology.json")
+    tp.write_text(json.dumps(topo, indent=4))
+    paths = {}
+    for short, full in BRS.items():
+        body = 'self = "%s"\ntopology = "%s"\ninternal_interfaces = [\n' % (full, tp)
+        body += ",\n".join('    {ip = "%s", port = 31002}' % a for a in internal[short]) + "\n]\n"
+        p = tmp_path / ("%s%s.toml" % (short, "_ipv6" if v6 else ""))
+        p.write_text(body)
+        paths[short] = p
+    # each namespace's addresses (the getifaddrs view): vethN holds the addresses configured on it
+    if_addrs = {}
+    for short in BRS:
+        m = {}
+        for ifid, veth, _ in TP._BRS[short]["ext"]:
+            m[ext(ifid, 2)] = "veth%d" % veth
+        for (veth, _), a in zip(TP._BRS[short]["int"], internal[short]):
+            m[a] = "veth%d" % veth
+        if_addrs[short] = m
+    return paths, if_addrs
+
+
+def next_hops(short, v6):
+    """The next-hop table of scion_hfv.topology.br_config, as (prefix, len, ifname, smac, dmac)."""
+    cfg = TP.br_config(short, v6)
+    out = []
+    for i in range(cfg.n_routes):
+        r = cfg.routes[i]
+        n = 16 if r.family == hfv.AF_INET6 else 4
+        import ipaddress
+        pfx = str(ipaddress.ip_address(bytes(r.prefix[:n])))
+        out.append((pfx, r.prefix_len, "veth%d" % r.ifindex, ":".join("%02x" % b for b in r.smac),
+                    ":".join("%02x" % b for b in r.dmac)))
+    return out
+
+
+def _entries(cfg, table, count):
+    arr = getattr(cfg, table)
+    return sorted(bytes(memoryview(arr[i]).cast("B")) for i in range(getattr(cfg, count)))
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+def test_loader_builds_the_reference_tables(tmp_path, v6):
+    paths, if_addrs = write_topology(tmp_path, v6)
+    ifindex = lambda name: int(name[4:])   # noqa: E731
+    built = {}
+    for short in BRS:
+        err = io.StringIO()
+        setup = C.load_config(str(paths[short]), if_addrs=if_addrs[short], err=err)
+        assert setup is not None and err.getvalue() == ""
+        cfg = C.build_tables(setup, ifindex, next_hops(short, v6))
+        ref = TP.br_config(short, v6)
+        for table, count in (("ingress", "n_ingress"), ("egress", "n_egress"), ("int_ifaces", "n_int_ifaces"),
+                             ("routes", "n_routes")):
+            assert _entries(cfg, table, count) == _entries(ref, table, count), (short, table)
+        assert sorted(cfg.tx_ports[:cfg.n_tx_ports]) == sorted(ref.tx_ports[:ref.n_tx_ports])
+        built[short] = T.OracleBR(cfg)
+    # and they route the PTF scenarios exactly like the reference expects
+    for name, kind, frame, first, ifi, want, veth_out in F.ptf_cases(v6, MAC):
+        out, last, egress, trace = T.run_chain(built, frame, first, ifi)
+        assert out == want and egress == veth_out, (name, kind)
+
+
+def test_listing_matches_br_loader(tmp_path):
+    paths, if_addrs = write_topology(tmp_path, False)
+    s = C.load_config(str(paths["br1"]), if_addrs=if_addrs["br1"])
+    assert str(s) == (
+        "XDP Border Router br1-ff00_0_1-1\n"
+        "External interfaces:\n"
+        "    1  veth1 local  [10.1.1.2]:50000\n"
+        "             remote [10.1.1.1]:50000\n"
+        "    2  veth3 local  [10.1.2.2]:50000\n"
+        "             remote [10.1.2.1]:50000\n"
+        "Sibling BR interfaces:\n"
+        "    3 route to [10.2.0.0]:31002\n"
+        "    4 route to [10.2.0.0]:31002\n"
+        "    5 route to [10.2.0.2]:31002\n"
+        "    6 route to [10.2.0.2]:31002\n"
+        "Internal interfaces:\n"
+        " veth5 [10.2.0.1]:31002\n"
+        " veth7 [10.2.0.3]:31002\n")
+
+
+def _load(tmp_path, toml_text, topo=None, if_addrs=None):
+    tp = tmp_path / "topo.json"
+    tp.write_text(json.dumps(topo if topo is not None else {"border_routers": {}}))
+    p = tmp_path / "c.toml"
+    p.write_text(toml_text.replace("@TOPO@", str(tp)))
+    err = io.StringIO()
+    return C.load_config(str(p), if_addrs=if_addrs or {}, err=err), err.getvalue()
+
+
+def test_loader_errors(tmp_path):
+    intf = 'internal_interfaces = [ {ip = "10.2.0.1", port = 31002} ]\n'
+    s, e = _load(tmp_path, 'topology = "@TOPO@"\n' + intf)
+    assert s is None and "'self' is missing" in e
+    s, e = _load(tmp_path, 'self = "a"\n' + intf)
+    assert s is None and "'topology' is missing" in e
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "/nonexistent/t.json"\n' + intf)
+    assert s is None and "File not found: /nonexistent/t.json" in e
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\n')
+    assert s is None and "'internal_interfaces' is missing" in e
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\ninternal_interfaces = [ {port = 1} ]\n')
+    assert s is None and "missing an IP address" in e
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\ninternal_interfaces = [ {ip = "10.0.0.1"} ]\n')
+    assert s is None and "missing the UDP port" in e
+    s, e = _load(tmp_path, 'self = "a" = 1\n')
+    assert s is None and "Parsing configuration failed" in e
+    mixed = {"border_routers": {"a": {"internal_addr": "10.0.0.1:1", "interfaces": {
+        "1": {"underlay": {"public": "10.0.0.1:50000", "remote": "[::1]:50000"}}}}}}
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\n' + intf, topo=mixed)
+    assert s is None and "same IP version" in e
+    badport = {"border_routers": {"a": {"internal_addr": "10.0.0.1:1", "interfaces": {
+        "1": {"underlay": {"public": "10.0.0.1:99999", "remote": "10.0.0.2:50000"}}}}}}
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\n' + intf, topo=badport)
+    assert s is None and "Parsing topology file failed" in e
+    ok = {"border_routers": {"a": {"internal_addr": "10.0.0.1:1", "interfaces": {
+        "1": {"underlay": {"public": "10.0.0.1:50000", "remote": "10.0.0.2:50000"}}}}}}
+    s, e = _load(tmp_path, 'self = "a"\ntopology = "@TOPO@"\n' + intf, topo=ok)
+    assert s is not None
+    assert "WARNING: No interface has IP 10.0.0.1\n         Cannot forward packets to IFID 1" in e
+    assert "WARNING: No interface has IP 10.2.0.1" in e
+    cfg = C.build_tables(s, lambda n: 1)
+    assert (cfg.n_ingress, cfg.n_egress, cfg.n_int_ifaces, cfg.n_tx_ports) == (0, 1, 0, 0)
+
+
+def test_parse_udp_ep():
+    ep = C.parse_udp_ep("[fd00:f00d:cafe::1]:31002")
+    assert str(ep.ip) == "fd00:f00d:cafe::1" and ep.port == 31002
+    assert C.parse_udp_ep("10.1.1.2:50000").port == 50000
+    for bad in ("10.1.1.2", "10.1.1.2:x", "300.1.1.1:1", "10.1.1.2:65536"):
+        with pytest.raises(C.ConfigError):
+            C.parse_udp_ep(bad)
+
+
+def test_stats_view():
+    st = np.zeros((64, 2, 11), dtype=np.uint64)
+    st[1, 0, 1], st[1, 1, 1] = 138 * 1000, 1000
+    st[1, 0, 10], st[1, 1, 10] = 138 * 7, 7
+    cur = S.port_totals(st, 1)
+    prev = S.port_totals(np.zeros_like(st), 1)
+    text = S.format_stats(cur, S.rates(cur, prev, 0.5))
+    lines = text.splitlines()
+    assert lines[0] == "Verdict             Packets    pkts/s         Bytes    Mbit/s"
+    assert lines[2] == "Forwarded             1000       2000        138000     2.208"
+    assert lines[11] == "Invalid HF               7         14           966  0.015456"
+    assert lines[1] == "Undefined                0          0             0         0"
+    assert ctypes.sizeof(ctypes.c_uint64) * st.size == 64 * 2 * 11 * 8

@@ -171,6 +171,7 @@ int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t 
 #define HFV_BR_MAX_TXPORTS 128
 #define HFV_BR_COUNTERS 11         /* enum counter (common.h:40-53) */
 #define HFV_BR_STATS_IFINDEX 64    /* counters kept for ingress ifindex < 64 */
+#define HFV_BR_ACTION_RETRY 0xff   /* internal to the windowed host path; never returned */
 
 struct hfv_br_int_iface {          /* int_iface_map: ifindex -> internal address (common.h:116-128) */
     uint32_t ifindex;
@@ -225,6 +226,22 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
 int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex,
                    size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats,
                    void *stream);
+/* Config 5: frames in HOST memory (an RX ring of `slot`-byte slots).  Chunk by chunk, only
+ * the first `window` bytes of each slot cross PCIe (strided DMA straight from `frames`;
+ * register the ring once with hfv_host_register so no bounce copy is needed), are processed
+ * exactly as hfv_br_process does, and the rewritten window is copied back in place.  Frames
+ * whose headers reach past the window are run again with the whole slot, so the result is
+ * identical to hfv_br_process on the full frames.  len, ingress_ifindex, action, verdict,
+ * egress_ifindex and stats (nullable, added to) are host arrays.  window: multiple of 8 with
+ * 64 <= window <= slot, or 0 for 256 (capped at slot).  Synchronous: on return every output
+ * is in host memory. */
+int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,
+                        const uint32_t *ingress_ifindex, size_t n, size_t window, uint8_t *action,
+                        uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats);
+/* Page-lock an existing host buffer (e.g. the RX ring) for direct DMA by this ctx's GPU. */
+int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes);
+int hfv_host_unregister(hfv_ctx *ctx, void *ptr);
+
 /* Same, then waits for the launch and returns its execution time (start/stop of the kernel
  * dispatch itself) in *kernel_ms.  For benchmarks. */
 int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len,

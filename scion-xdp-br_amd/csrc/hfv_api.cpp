@@ -160,6 +160,12 @@ struct hfv_ctx {
     hipEvent_t tev[2] = {nullptr, nullptr};
     // router tables for hfv_br_process (published with the key table)
     DevBrConfig br{};
+    // windowed host path (hfv_br_process_host): per-stream device/pinned chunk buffers
+    size_t brh_win_cap = 0;               // bytes per frame the device windows hold
+    uint8_t *brh_dwin[2] = {nullptr, nullptr};
+    uint8_t *brh_dio[2] = {nullptr, nullptr};   // len u16 | ifindex u32 | action u8 | verdict u8 | egress i32
+    uint8_t *brh_hio[2] = {nullptr, nullptr};   // pinned twin of brh_dio
+    uint64_t *brh_dstats = nullptr;
 };
 
 // NULL is HIP's default stream, as for any HIP API taking a stream.
@@ -294,6 +300,12 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->tab_done[i]) { (void)hipEventSynchronize(ctx->tab_done[i]); (void)hipEventDestroy(ctx->tab_done[i]); }
         if (ctx->dev_tab[i]) (void)hipFree(ctx->dev_tab[i]);
     }
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
+        if (ctx->brh_dio[i]) (void)hipFree(ctx->brh_dio[i]);
+        if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
+    }
+    if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
     keymap_close(ctx->keymap);
     for (int i = 0; i < 2; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
@@ -392,6 +404,12 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
         if (!rc) rc = keymap_open_ro(path, &m);
     }
     if (rc) return fail(rc, "cannot attach key map %s", path);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
+        if (ctx->brh_dio[i]) (void)hipFree(ctx->brh_dio[i]);
+        if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
+    }
+    if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
     keymap_close(ctx->keymap);
     ctx->keymap = m;
     strcpy(ctx->keymap_path, path);
@@ -623,8 +641,8 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
     DevState *ds;
     rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, pkts, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex,
-                              stats, st);
+    int e = launch_br_process(ctx->geom, ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
+                              action, verdict, egress_ifindex, stats, st);
     return after_launch(ctx, st, e, "br_process launch");
 }
 
@@ -645,12 +663,164 @@ int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_
     DevState *ds;
     rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, pkts, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex,
-                              stats, st, ctx->tev[0], ctx->tev[1]);
+    int e = launch_br_process(ctx->geom, ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
+                              action, verdict, egress_ifindex, stats, st, ctx->tev[0], ctx->tev[1]);
     rc = after_launch(ctx, st, e, "br_process launch");
     if (rc) return rc;
     HIP_TRY(hipEventSynchronize(ctx->tev[1]));
     HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
+// Windowed host path.  Per chunk of kBrChunk frames, on alternating streams: strided H2D of
+// the windows + metadata, the kernel (stride = window, lengths clamped to the caller's slot),
+// strided D2H of the rewritten windows + results.  Then frames marked HFV_BR_ACTION_RETRY
+// (headers beyond the window) go through again with whole slots.
+static const size_t kBrChunk = (size_t)1 << 16;
+
+static int brh_buffers(hfv_ctx *ctx, size_t window)
+{
+    for (int i = 0; i < 2; ++i) {
+        if (!ctx->hstream[i]) HIP_TRY(hipStreamCreateWithFlags(&ctx->hstream[i], hipStreamNonBlocking));
+        if (!ctx->brh_dio[i]) {
+            HIP_TRY(hipMalloc((void **)&ctx->brh_dio[i], kBrChunk * 12));
+            HIP_TRY(hipHostMalloc((void **)&ctx->brh_hio[i], kBrChunk * 12, hipHostMallocDefault));
+        }
+    }
+    if (!ctx->brh_dstats) HIP_TRY(hipMalloc((void **)&ctx->brh_dstats, HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8));
+    if (ctx->brh_win_cap < window) {
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipStreamSynchronize(ctx->hstream[i]));
+            if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
+            ctx->brh_dwin[i] = nullptr;
+            HIP_TRY(hipMalloc((void **)&ctx->brh_dwin[i], kBrChunk * window));
+        }
+        ctx->brh_win_cap = window;
+    }
+    return 0;
+}
+
+// One chunk: frames[k * fstride] for k < cnt (window bytes each), metadata through pinned io.
+static int brh_chunk(hfv_ctx *ctx, int sl, uint8_t *frames, size_t fstride, size_t maxlen, size_t window,
+                     const uint16_t *len, const uint32_t *ifx, size_t cnt)
+{
+    hipStream_t st = ctx->hstream[sl];
+    uint8_t *hio = ctx->brh_hio[sl], *dio = ctx->brh_dio[sl];
+    memcpy(hio, len, cnt * 2);
+    memcpy(hio + kBrChunk * 2, ifx, cnt * 4);
+    HIP_TRY(hipMemcpyAsync(dio, hio, kBrChunk * 6, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpy2DAsync(ctx->brh_dwin[sl], window, frames, fstride, window, cnt, hipMemcpyHostToDevice, st));
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_br_process(ctx->geom, ds, ctx->brh_dwin[sl], window, (uint32_t)maxlen, (uint32_t)window,
+                              (const uint16_t *)dio, (const uint32_t *)(dio + kBrChunk * 2), cnt,
+                              dio + kBrChunk * 6, dio + kBrChunk * 7, (int32_t *)(dio + kBrChunk * 8),
+                              ctx->brh_dstats, st);
+    rc = after_launch(ctx, st, e, "br_process launch");
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy2DAsync(frames, fstride, ctx->brh_dwin[sl], window, window, cnt, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hio + kBrChunk * 6, dio + kBrChunk * 6, kBrChunk * 6, hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+static void brh_results(hfv_ctx *ctx, int sl, size_t cnt, uint8_t *action, uint8_t *verdict, int32_t *egress)
+{
+    const uint8_t *hio = ctx->brh_hio[sl];
+    memcpy(action, hio + kBrChunk * 6, cnt);
+    memcpy(verdict, hio + kBrChunk * 7, cnt);
+    memcpy(egress, hio + kBrChunk * 8, cnt * 4);
+}
+
+int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,
+                        const uint32_t *ingress_ifindex, size_t n, size_t window, uint8_t *action,
+                        uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats)
+{
+    if (n == 0) return ctx ? 0 : fail(-EINVAL, "ctx is NULL");
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (!frames || !len || !ingress_ifindex || !action || !verdict || !egress_ifindex) return fail(-EINVAL, "null buffer");
+    if (slot < 64 || (slot & 7) || slot > 65535 * 8) return fail(-EINVAL, "slot must be >= 64 and a multiple of 8");
+    if (window == 0) window = slot < 256 ? slot : 256;
+    if (window < 64 || (window & 7) || window > slot) return fail(-EINVAL, "window must be a multiple of 8 in [64, slot]");
+    DeviceGuard g(ctx->device);
+    int rc = brh_buffers(ctx, window > slot ? slot : window);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->brh_dstats, 0, HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8, ctx->hstream[0]));
+    HIP_TRY(hipStreamSynchronize(ctx->hstream[0]));
+    size_t nchunks = (n + kBrChunk - 1) / kBrChunk;
+    size_t first_of[2] = {0, 0}, cnt_of[2] = {0, 0};
+    for (size_t c = 0; c < nchunks + 2; ++c) {
+        int sl = (int)(c & 1);
+        if (c >= 2) {
+            HIP_TRY(hipStreamSynchronize(ctx->hstream[sl]));
+            size_t f = first_of[sl];
+            brh_results(ctx, sl, cnt_of[sl], action + f, verdict + f, egress_ifindex + f);
+        }
+        if (c >= nchunks) continue;
+        size_t first = c * kBrChunk, cnt = n - first < kBrChunk ? n - first : kBrChunk;
+        rc = brh_chunk(ctx, sl, frames + first * slot, slot, slot, window, len + first, ingress_ifindex + first, cnt);
+        if (rc) return rc;
+        first_of[sl] = first;
+        cnt_of[sl] = cnt;
+    }
+    // frames whose headers did not fit the window: whole slots, in chunks, through a bounce buffer
+    size_t nretry = 0;
+    for (size_t i = 0; i < n; ++i) nretry += action[i] == HFV_BR_ACTION_RETRY;
+    if (nretry) {
+        rc = brh_buffers(ctx, slot);
+        if (rc) return rc;
+        uint8_t *bounce = nullptr;
+        size_t cap = nretry < kBrChunk ? nretry : kBrChunk;
+        HIP_TRY(hipHostMalloc((void **)&bounce, cap * slot + cap * 8, hipHostMallocDefault));
+        uint16_t *blen = (uint16_t *)(bounce + cap * slot);
+        uint32_t *bif = (uint32_t *)(bounce + cap * slot + cap * 2);
+        size_t *idx = (size_t *)malloc(cap * sizeof(size_t));
+        size_t i = 0;
+        while (rc == 0 && i < n) {
+            size_t cnt = 0;
+            for (; i < n && cnt < cap; ++i) {
+                if (action[i] != HFV_BR_ACTION_RETRY) continue;
+                memcpy(bounce + cnt * slot, frames + i * slot, slot);
+                blen[cnt] = len[i];
+                bif[cnt] = ingress_ifindex[i];
+                idx[cnt++] = i;
+            }
+            if (!cnt) break;
+            rc = brh_chunk(ctx, 0, bounce, slot, slot, slot, blen, bif, cnt);
+            if (rc == 0 && hipStreamSynchronize(ctx->hstream[0]) != hipSuccess) rc = fail(-EIO, "retry chunk");
+            for (size_t k = 0; rc == 0 && k < cnt; ++k) {
+                size_t j = idx[k];
+                memcpy(frames + j * slot, bounce + k * slot, slot);
+                action[j] = ctx->brh_hio[0][kBrChunk * 6 + k];
+                verdict[j] = ctx->brh_hio[0][kBrChunk * 7 + k];
+                memcpy(&egress_ifindex[j], ctx->brh_hio[0] + kBrChunk * 8 + 4 * k, 4);
+            }
+        }
+        free(idx);
+        (void)hipHostFree(bounce);
+        if (rc) return rc;
+    }
+    if (stats) {
+        uint64_t tmp[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+        HIP_TRY(hipMemcpy(tmp, ctx->brh_dstats, sizeof tmp, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < sizeof tmp / 8; ++k) stats[k] += tmp[k];
+    }
+    return 0;
+}
+
+int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes)
+{
+    if (!ctx || !ptr || !bytes) return fail(-EINVAL, "bad argument");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return 0;
+}
+
+int hfv_host_unregister(hfv_ctx *ctx, void *ptr)
+{
+    if (!ctx || !ptr) return fail(-EINVAL, "bad argument");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipHostUnregister(ptr));
     return 0;
 }
 

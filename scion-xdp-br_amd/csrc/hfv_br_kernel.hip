@@ -59,6 +59,9 @@ __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(
 struct BrFrame {
     uint8_t *p;
     int len;
+    int lim;           // bytes of the frame present in the buffer (min(len, window))
+    bool cut;          // a check failed only because the window ended before len
+
     uint32_t ifindex;
     uint32_t last_verdict;
     int ip, udp, meta, inf, hf;
@@ -79,12 +82,22 @@ struct BrFrame {
     uint32_t mac_lo, mac_hi;
 };
 
+// Bounds check of the BPF code ("data + n > data_end").  With a header window smaller than the
+// frame, running past the window marks the frame `cut` (the host path re-runs it whole).
+__device__ __forceinline__ bool beyond(BrFrame &k, int end)
+{
+    if (end <= k.lim) return false;
+    if (end <= k.len) k.cut = true;
+    return true;
+}
+
 template <bool STATS>
 __device__ __forceinline__ uint32_t record(BrFrame &k, uint32_t verdict)   // record_verdict, xdp.c:54-70
 {
     uint32_t idx = (verdict >> 3) & 0x0fu;
     k.last_verdict = verdict;
     if constexpr (STATS) {
+        if (k.cut) return verdict & 7u;
         if (k.ifindex < HFV_BR_STATS_IFINDEX && idx < HFV_BR_COUNTERS) {
             unsigned long long *row = s_stats + k.ifindex * 2 * HFV_BR_COUNTERS;
             atomicAdd(row + idx, (unsigned long long)k.len);
@@ -99,12 +112,12 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
 {
     k.verdict = V_NOT_SCION;
     int off = 14;
-    if (off > k.len) return -1;
+    if (beyond(k, off)) return -1;
     uint32_t proto = g16(k.p + 12);
     if (proto == 0x0008u) {   // ETH_P_IP, network order
         k.ip = off;
         off += 20;
-        if (off > k.len) return -1;
+        if (beyond(k, off)) return -1;
         const uint8_t *ip = k.p + k.ip;
         k.family = HFV_AF_INET;
         k.v4_dst = g32(ip + 16);
@@ -121,7 +134,7 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
     } else if (proto == 0xdd86u) {   // ETH_P_IPV6
         k.ip = off;
         off += 40;
-        if (off > k.len) return -1;
+        if (beyond(k, off)) return -1;
         const uint8_t *ip = k.p + k.ip;
         k.family = HFV_AF_INET6;
 #pragma unroll
@@ -138,7 +151,7 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
     }
     k.udp = off;
     off += 8;
-    if (off > k.len) return -1;
+    if (beyond(k, off)) return -1;
     k.udp_dst = g16(k.p + k.udp + 2);
     k.udp_residual -= k.udp_dst;
     k.udp_src = g16(k.p + k.udp);
@@ -151,7 +164,7 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     k.verdict = V_PARSE_ERROR;
     k.meta = off;
     off += 4;
-    if (off > k.len) return -1;
+    if (beyond(k, off)) return -1;
     uint32_t raw = g32(k.p + k.meta);
     k.udp_residual -= raw;
     k.h_meta = sw32(raw);
@@ -163,16 +176,16 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     k.curr_hf = (k.h_meta >> 24) & 0x3fu;
     int inf = off + (int)k.curr_inf * 8;
     k.inf = inf;
-    if (inf + 8 > k.len) return -1;
+    if (beyond(k, inf + 8)) return -1;
     k.seg_id0 = g16(k.p + inf + 2);
     k.udp_residual -= k.seg_id0;
     if (k.curr_inf + 1 < k.num_inf) {
         inf += 8;
-        if (inf + 8 > k.len) return -1;
+        if (beyond(k, inf + 8)) return -1;
         k.seg_id1 = g16(k.p + inf + 2);
     }
     k.hf = off + (int)k.num_inf * 8 + (int)k.curr_hf * 12;
-    if (k.hf + 12 > k.len) return -1;
+    if (beyond(k, k.hf + 12)) return -1;
     return off;
 }
 
@@ -181,14 +194,14 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
     k.verdict = V_PARSE_ERROR;
     int sc = off;
     off += 28;
-    if (off > k.len) return -1;
+    if (beyond(k, off)) return -1;
     if ((g8(k.p + sc) >> 4) != 0) {
         k.verdict = V_NOT_IMPLEMENTED;
         return -1;
     }
     uint32_t haddr = g8(k.p + sc + 9);
     off += 8 + 4 * (int)((haddr >> 2) & 0x2u) + 4 * (int)((haddr >> 6) & 0x2u);   // SC_GET_DL/SL, scion.h:49-52
-    if (off > k.len) return -1;
+    if (beyond(k, off)) return -1;
     k.path_type = g8(k.p + sc + 8);
     if (k.path_type == 1u) return parse_scion_path(k, off);
     k.verdict = V_NOT_IMPLEMENTED;
@@ -234,7 +247,7 @@ __device__ __forceinline__ bool as_ingress(BrFrame &k)
         ++k.curr_inf;
         ++k.curr_hf;
         k.hf += 12;
-        if (k.hf + 12 > k.len) {
+        if (beyond(k, k.hf + 12)) {
             k.verdict = V_PARSE_ERROR;
             return false;
         }
@@ -253,7 +266,7 @@ __device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
     int inf = k.inf;
     if (k.segment_switch) {
         inf += 8;
-        if (inf + 8 > k.len) return false;
+        if (beyond(k, inf + 8)) return false;
     }
     uint32_t beta = sw16(k.segment_switch ? k.seg_id1 : k.seg_id0);
     if (as_ing_ifid == 0) defer_verify(k, k.inf, k.hf, sw16(beta));   // original INF, path_processing.h:142
@@ -493,7 +506,7 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
     int inf = k.inf;
     if (k.segment_switch) {
         inf += 8;
-        if (inf + 8 > k.len) return 0;
+        if (beyond(k, inf + 8)) return 0;
     }
     const uint8_t *hf = k.p + k.hf;
     uint32_t key = sw16(cons_at(k, inf) ? g16(hf + 4) : g16(hf + 2));
@@ -528,7 +541,8 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 template <int BLOCK, bool STATS>
 __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st,
                                                       const uint32_t *__restrict__ ttab_img, uint8_t *pkts,
-                                                      uint64_t slot, const uint16_t *__restrict__ lens,
+                                                      uint64_t slot, uint32_t maxlen, uint32_t window,
+                                                      const uint16_t *__restrict__ lens,
                                                       const uint32_t *__restrict__ ifidx, uint64_t n,
                                                       uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
                                                       int32_t *__restrict__ egress,
@@ -551,9 +565,16 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         BrFrame k = {};
         k.p = pkts + i * slot;
         uint32_t len = lens[i];
-        k.len = (int)(len <= slot ? len : slot);
+        k.len = (int)(len <= maxlen ? len : maxlen);
+        k.lim = k.len < (int)window ? k.len : (int)window;
         k.ifindex = ifidx[i];
         int a = process_packet<STATS>(k);
+        if (k.cut) {   // headers reach past the window: untouched, uncounted, caller re-runs it whole
+            action[i] = HFV_BR_ACTION_RETRY;
+            verdict[i] = 0;
+            egress[i] = -1;
+            continue;
+        }
         if (a <= 0) {
             // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
             uint32_t v = A_ABORTED;
@@ -582,16 +603,17 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
 
 constexpr int kBrBlock = 1024;
 
-int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, const uint16_t *len,
-                      const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
-                      int32_t *egress_ifindex, uint64_t *stats, void *stream, void *ev_start, void *ev_stop)
+int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
+                      uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                      uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
+                      void *ev_start, void *ev_stop)
 {
     uint64_t blocks = (n + kBrBlock - 1) / kBrBlock;
     uint64_t cap = (uint64_t)g.num_cus;   // one 1024-thread block per CU (LDS: tables + counters)
     unsigned grid = (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
     auto k = stats ? k_br_process<kBrBlock, true> : k_br_process<kBrBlock, false>;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBrBlock), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, len,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, maxlen, window, len,
                           ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
                           (unsigned long long *)stats);
     return (int)hipGetLastError();

@@ -108,10 +108,12 @@ int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uin
                           uint64_t *bits, uint64_t *stamps, void *stream);
 int build_ttab_image(uint32_t *img, void *stream);
 // full border-router path (hfv_br_kernel.hip)
-int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, const uint16_t *len,
-                      const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
-                      int32_t *egress_ifindex, uint64_t *stats, void *stream, void *ev_start = nullptr,
-                      void *ev_stop = nullptr);
+// slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
+// slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).
+int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
+                      uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                      uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
+                      void *ev_start = nullptr, void *ev_stop = nullptr);
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);

@@ -75,6 +75,9 @@ def lib():
         "hfv_br_set_config": (i32, [vp, vp]),
         "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
+        "hfv_br_process_host": (i32, [vp, vp, sz, vp, vp, sz, sz, vp, vp, vp, vp]),
+        "hfv_host_register": (i32, [vp, vp, sz]),
+        "hfv_host_unregister": (i32, [vp, vp]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
         "hfv_expand_keys": (i32, [vp, vp, sz, vp, vp]),
@@ -266,6 +269,18 @@ class Ctx:
                    stream=None):
         _check(lib().hfv_br_process(self._h, _ptr(pkts), slot, _ptr(lens), _ptr(ingress_ifindex), n, _ptr(action),
                                     _ptr(verdict), _ptr(egress_ifindex), _ptr(stats), _stream(stream)))
+
+    def br_process_host(self, frames, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
+                        window=0):
+        """Config 5: numpy host arrays in, results in place (hfv_br_process_host)."""
+        _check(lib().hfv_br_process_host(self._h, _ptr(frames), slot, _ptr(lens), _ptr(ingress_ifindex), n, window,
+                                         _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats)))
+
+    def host_register(self, buf):
+        _check(lib().hfv_host_register(self._h, _ptr(buf), buf.nbytes))
+
+    def host_unregister(self, buf):
+        _check(lib().hfv_host_unregister(self._h, _ptr(buf)))
 
     def br_process_timed(self, pkts, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
                          stream=None):

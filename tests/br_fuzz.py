@@ -46,6 +46,32 @@ def hop_inputs(brs, v6, mac_fn, seeds=(0x1234, 0xBEEF, 0x0001)):
     return res
 
 
+def long_path_frames(v6, mac_fn, count=8):
+    """Frames BR 1 verifies and forwards whose current hop field lies deep in a 3-segment path
+    (past byte 256), for the header-window overflow of the host path.  The current hop is hop
+    j of segment 1 (Cons), so the SegID the frame carries is beta_j of that segment."""
+    import struct as _s
+    from scion_hfv import topology as TP
+    out = []
+    for k in range(count):
+        ing_enc, _, _, ifi = TP.encaps(1, 2, v6)
+        lens = [12 + k, 20, 10]
+        j = 3 + k
+        cur = lens[0] + j
+        hops = [P.HopField(3, 4) for _ in range(sum(lens))]
+        hops[cur] = P.HopField(1, 2)
+        keys = [TP.KEYS[(i % 8) + 2] for i in range(len(hops))]
+        keys[cur] = TP.KEYS[1]
+        p = P.Path([P.InfoField(False), P.InfoField(True), P.InfoField(False)], hops, lens, mac_fn=mac_fn)
+        p.init_macs(keys, [0x11 * k, 0x22 + k, 0x33])
+        for h in hops[lens[0]:cur]:
+            p.infos[1].seg_id ^= _s.unpack(">H", h.mac[:2])[0]
+        p.curr_inf, p.curr_hf = 1, cur
+        assert p.verify_current(TP.KEYS[1])
+        out.append((ing_enc.frame(P.scion_header(p.pack())), ifi))
+    return out
+
+
 IFINDICES = [1, 3, 4, 5, 6, 7, 9, 11, 13, 15, 2, 63, 64, 200]
 
 

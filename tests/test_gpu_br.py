@@ -98,3 +98,56 @@ def test_stats_accumulate_and_bad_args(gpu_ctx):
     cfg.n_routes = 65
     with pytest.raises(hfv.HfvError):
         gpu_ctx.br_set_config(cfg)
+
+
+@pytest.mark.parametrize("window", [64, 256, 0])
+def test_host_path_matches_oracle(gpu_ctx, window):
+    """Config 5 (hfv_br_process_host): frames in host memory, only a header window crosses
+    PCIe; frames whose headers pass the window (long paths, and for window 64 nearly all) are
+    re-run whole.  Result identical to the oracle on the full frames."""
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 70000, seed=21, payload_max=1500)
+    longf = F.long_path_frames(False, MAC)
+    for k, (f, ifi) in enumerate(longf):   # sprinkle long-path frames over both chunks
+        i = 1000 + k * 8191
+        frames[i] = 0
+        frames[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+        lens[i], ifidx[i] = len(f), ifi
+    ref = frames.copy()
+    oa, ov, oe, os_ = orc.br_process(ref, lens, ifidx, T.br_config("br1"), orc.hop_key(T.KEYS[1]))
+    gpu_ctx.br_set_config(T.br_config("br1"))
+    gpu_ctx.key_add(0, T.KEYS[1])
+    n = len(frames)
+    got = frames.copy()
+    a = np.zeros(n, np.uint8)
+    v = np.zeros(n, np.uint8)
+    e = np.zeros(n, np.int32)
+    st = np.zeros((64, 2, 11), np.uint64)
+    gpu_ctx.host_register(got)
+    try:
+        gpu_ctx.br_process_host(got, T.SLOT, lens, ifidx, n, a, v, e, st, window=window)
+    finally:
+        gpu_ctx.host_unregister(got)
+    assert (a == oa).all() and (v == ov).all() and (e == oe).all()
+    assert (got == ref).all()
+    assert (st == os_).all()
+    assert (a[[1000 + k * 8191 for k in range(len(longf))]] == 4).all()
+
+
+def test_host_path_pageable_and_args(gpu_ctx):
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 3000, seed=5, slot=512)
+    ref = frames.copy()
+    oa, ov, oe, _ = orc.br_process(ref, lens, ifidx, T.br_config("br1"), orc.hop_key(T.KEYS[1]))
+    gpu_ctx.br_set_config(T.br_config("br1"))
+    gpu_ctx.key_add(0, T.KEYS[1])
+    a = np.zeros(3000, np.uint8)
+    v = np.zeros(3000, np.uint8)
+    e = np.zeros(3000, np.int32)
+    gpu_ctx.br_process_host(frames, 512, lens, ifidx, 3000, a, v, e, None, window=128)   # not registered
+    assert (a == oa).all() and (v == ov).all() and (e == oe).all() and (frames == ref).all()
+    for bad in (60, 1024, 100):
+        with pytest.raises(hfv.HfvError):
+            gpu_ctx.br_process_host(frames, 512, lens, ifidx, 3000, a, v, e, None, window=bad)

@@ -26,6 +26,12 @@ AS ingress/egress, next hop, rewrite, MAC check, counters) as BR 1 of the refere
 topology, over n frames of 64..1500 B in 2 KiB slots (PTF scenario traffic, 1/16 with a
 corrupted hop-field MAC).  Frames are rewritten in place, so each timed step gets its own
 pristine copy of the batch (K copies resident in HBM, made before the timed region).
+
+    python bench.py --workload br-host [--n 1048576] [--steps 5] [--window 256]
+
+runs config 5: the same frames start and end in (registered) host memory; per step one
+hfv_br_process_host call moves the header windows over PCIe, processes them and writes the
+rewritten windows back.  Each step's input is restored (untimed) before it runs.
 """
 import argparse
 import json
@@ -229,14 +235,7 @@ def run_br(args, rank, world, local):
     ctx.br_set_config(cfg)
     stream = torch.cuda.current_stream().cuda_stream
     frames, ifis, good, abytes = br_templates()
-    nt = len(frames) // 2
-    rng = np.random.default_rng(0x5C100004 + rank)
-    tid = (np.arange(n) % nt) * 2 + corrupted(n, rank * n)          # template = 2 * flow + bad
-    hdr = np.array([len(f) for f in frames])
-    lens = np.maximum(hdr[tid], rng.integers(64, 1501, n)).astype(np.uint16)
-    tmpl = np.zeros((len(frames), BR_SLOT), dtype=np.uint8)
-    for i, f in enumerate(frames):
-        tmpl[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+    tmpl, tid, lens, _, n_good = br_batch(n, rank)
     d_tid = torch.from_numpy(tid.astype(np.int64)).cuda()
     master = torch.from_numpy(tmpl).cuda()[d_tid]                    # n x 2 KiB, gathered on device
     d_len = torch.from_numpy(lens.view(np.int16)).cuda()
@@ -245,7 +244,6 @@ def run_br(args, rank, world, local):
     ver = torch.zeros_like(act)
     egr = torch.zeros(n, dtype=torch.int32, device="cuda")
     stats = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
-    n_good = int(np.array(good)[tid].sum())
     alg = float(np.array(abytes)[tid].mean())
 
     work = torch.empty_like(master)
@@ -307,19 +305,90 @@ def run_br(args, rank, world, local):
         dist.destroy_process_group()
 
 
+def br_batch(n, rank):
+    """Host copy of the config-4 batch: frames [n, 2 KiB], lengths, ingress ifindex, #good."""
+    frames, ifis, good, abytes = br_templates()
+    nt = len(frames) // 2
+    rng = np.random.default_rng(0x5C100004 + rank)
+    tid = (np.arange(n) % nt) * 2 + corrupted(n, rank * n)
+    hdr = np.array([len(f) for f in frames])
+    lens = np.maximum(hdr[tid], rng.integers(64, 1501, n)).astype(np.uint16)
+    tmpl = np.zeros((len(frames), BR_SLOT), dtype=np.uint8)
+    for i, f in enumerate(frames):
+        tmpl[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+    return tmpl, tid, lens, np.array(ifis, dtype=np.uint32)[tid], int(np.array(good)[tid].sum())
+
+
+def run_br_host(args, rank, world, local):
+    from scion_hfv import topology as TP
+    n, steps = args.n, args.steps
+    ctx = hfv.Ctx(local)
+    ctx.key_add(0, TP.KEYS[1])
+    ctx.br_set_config(TP.br_config("br1"))
+    tmpl, tid, lens, ifidx, n_good = br_batch(n, rank)
+    pristine = tmpl[tid]                                   # n x 2 KiB in host memory
+    frames = np.empty_like(pristine)
+    ctx.host_register(frames)
+    act = np.zeros(n, np.uint8)
+    ver = np.zeros(n, np.uint8)
+    egr = np.zeros(n, np.int32)
+    hdr = 256
+    for _ in range(max(1, args.warmup)):
+        frames[:] = pristine
+        ctx.br_process_host(frames, BR_SLOT, lens, ifidx, n, act, ver, egr, None, window=args.window)
+    assert int((act == 4).sum()) == n_good and int((ver == hfv.VERDICT["INVALID_HF"]).sum()) == n - n_good
+    total = 0.0
+    for _ in range(steps):
+        frames[:, :hdr] = pristine[:, :hdr]                # restore the rewritten headers (untimed)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ctx.br_process_host(frames, BR_SLOT, lens, ifidx, n, act, ver, egr, None, window=args.window)
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        total += dt
+    ctx.host_unregister(frames)
+    result = {
+        "metric": "Mpkt/s full border-router path with frames in host memory (H2D + kernel + D2H), "
+                  "mixed 64-1500 B frames",
+        "value": round(world * n * steps / total / 1e6, 2), "unit": "Mpkt/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": round(total / steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (the config-4 frame mix, 2 KiB slots in registered host memory)",
+        "config": {"workload": f"config 5: {n} host-resident frames per GPU through hfv_br_process_host",
+                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "window_bytes": args.window or 256,
+                   "pcie_bytes_per_frame": 2 * (args.window or 256) + 12,
+                   "parallelism": f"batch-sharded x{world}, no collective"},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="default 200 (hf), 10 (br), 5 (br-host)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 20 (hf), 3 (br), 1 (br-host)")
     ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU (config 2: 2^20)")
     ap.add_argument("--keysel", choices=["zero", "ifid"], default="zero")
     ap.add_argument("--big-n", type=int, default=1 << 24, help="HBM-resident run size (0 = skip)")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
     ap.add_argument("--no-host-e2e", action="store_true")
-    ap.add_argument("--workload", choices=["hf", "br"], default="hf",
-                    help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4")
+    ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
+                    help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
+                         "br-host: config 5")
+    ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = {"hf": 200, "br": 10, "br-host": 5}[args.workload]
+    if args.warmup is None:
+        args.warmup = {"hf": 20, "br": 3, "br-host": 1}[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -329,6 +398,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.workload == "br":
         return run_br(args, rank, world, local)
+    if args.workload == "br-host":
+        return run_br_host(args, rank, world, local)
     keysel = hfv.KEYSEL_IFID if args.keysel == "ifid" else hfv.KEYSEL_ZERO
     n = args.n
 

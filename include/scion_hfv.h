@@ -238,6 +238,15 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
 int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,
                         const uint32_t *ingress_ifindex, size_t n, size_t window, uint8_t *action,
                         uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats);
+/* ---- pinned verdict counters ----------------------------------------------------------
+ * A file-backed port_stats_map (maps.h; pinned by br_loader.cpp:136-140, read by
+ * `br-loader watch`, stats.cpp): $HFV_PIN_DIR/<br>/port_stats_map, same counter layout as the
+ * `stats` buffer of hfv_br_process.  The data path adds its counters after a batch;
+ * `hfv-loader watch <br> <iface>` prints them with per-second rates. */
+int hfv_statsmap_path(const char *br, char *out, size_t len);
+int hfv_statsmap_add(const char *path, const uint64_t *stats);   /* creates the map if needed */
+int hfv_statsmap_read(const char *path, uint64_t *stats);
+
 /* Page-lock an existing host buffer (e.g. the RX ring) for direct DMA by this ctx's GPU. */
 int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes);
 int hfv_host_unregister(hfv_ctx *ctx, void *ptr);

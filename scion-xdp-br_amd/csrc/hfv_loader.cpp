@@ -4,13 +4,19 @@
 //   hfv-loader key add <br> <index> <base64-key>    decode, expand, derive K1, update map
 //   hfv-loader key remove <br> <index>              erase the slot (it then fails closed)
 //   hfv-loader key list <br>                        print occupied slots and K1 of each
+//   hfv-loader watch <br> <iface> [seconds]         verdict counters of one ingress port,
+//                                                   every second (br_loader.cpp:162-180)
 //
 // The pinned map lives at $HFV_PIN_DIR/<br>/mac_key_map (default /dev/shm/hfv); a data plane
 // that called hfv_ctx_attach_keymap() on it picks the change up at its next batch.  Messages
 // and exit codes follow br-loader: errors on stderr, EXIT_FAILURE.
+#include <net/if.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <stdexcept>
 #include <string>
@@ -22,7 +28,8 @@ static void print_usage()
     fprintf(stderr,
             "Usage: hfv-loader key add <br> <index> <key>\n"
             "                  key remove <br> <index>\n"
-            "                  key list <br>\n");
+            "                  key list <br>\n"
+            "       hfv-loader watch <br> <iface> [seconds]\n");
 }
 
 static bool parse_index(const char *s, uint32_t *out)
@@ -112,8 +119,91 @@ static int list_keys(int argc, char **argv)
     return EXIT_SUCCESS;
 }
 
+// ---- watch (stats.cpp:38-144) ------------------------------------------------------------
+static const char *kStatNames[HFV_BR_COUNTERS] = {
+    "Undefined",       "Forwarded",     "Parse error",       "Not SCION",    "Not implemented", "No interface",
+    "Underlay mismatch", "Router alert", "FIB lookup drop", "FIB lookup pass", "Invalid HF",
+};
+
+static volatile sig_atomic_t g_stop = 0;
+static void on_sigint(int) { g_stop = 1; }
+
+static void print_stats(const uint64_t *bytes, const uint64_t *pkts, const double *rb, const double *rp)
+{
+    printf("Verdict             Packets    pkts/s         Bytes    Mbit/s\n");
+    for (int i = 0; i < HFV_BR_COUNTERS; ++i)
+        printf("%-18s%8llu%11.0f%14llu%10.5g\n", kStatNames[i], (unsigned long long)pkts[i], rp[i],
+               (unsigned long long)bytes[i], rb[i] * 8e-6);
+    fflush(stdout);
+}
+
+static bool port_totals(const char *path, uint32_t ifindex, uint64_t *bytes, uint64_t *pkts)
+{
+    static uint64_t all[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+    if (hfv_statsmap_read(path, all) != 0) return false;
+    memcpy(bytes, all + (size_t)ifindex * 2 * HFV_BR_COUNTERS, sizeof(uint64_t) * HFV_BR_COUNTERS);
+    memcpy(pkts, all + ((size_t)ifindex * 2 + 1) * HFV_BR_COUNTERS, sizeof(uint64_t) * HFV_BR_COUNTERS);
+    return true;
+}
+
+static double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static int watch(int argc, char **argv)
+{
+    if (argc < 2) { print_usage(); return EXIT_FAILURE; }
+    char path[4096];
+    if (hfv_statsmap_path(argv[0], path, sizeof path) != 0) {
+        fprintf(stderr, "Invalid border router name: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
+    uint32_t ifindex = if_nametoindex(argv[1]);
+    if (!ifindex && !parse_index(argv[1], &ifindex)) {
+        fprintf(stderr, "Unknown interface: %s\n", argv[1]);
+        return EXIT_FAILURE;
+    }
+    if (ifindex >= HFV_BR_STATS_IFINDEX) {
+        fprintf(stderr, "Lookup failed\n");
+        return EXIT_FAILURE;
+    }
+    uint32_t seconds = 0;   // 0: until SIGINT, like br-loader
+    if (argc >= 3 && !parse_index(argv[2], &seconds)) { print_usage(); return EXIT_FAILURE; }
+    uint64_t b[HFV_BR_COUNTERS], p[HFV_BR_COUNTERS], pb[HFV_BR_COUNTERS], pp[HFV_BR_COUNTERS];
+    double rb[HFV_BR_COUNTERS] = {0}, rp[HFV_BR_COUNTERS] = {0};
+    double t0 = now_s();
+    if (!port_totals(path, ifindex, b, p)) {
+        fprintf(stderr, "Lookup failed\n");
+        return EXIT_FAILURE;
+    }
+    print_stats(b, p, rb, rp);
+    signal(SIGINT, on_sigint);
+    for (uint32_t k = 0; !g_stop && (seconds == 0 || k < seconds); ++k) {
+        sleep(1);
+        if (g_stop) break;
+        double t1 = now_s(), dt = t1 - t0;
+        t0 = t1;
+        memcpy(pb, b, sizeof b);
+        memcpy(pp, p, sizeof p);
+        if (!port_totals(path, ifindex, b, p)) {
+            fprintf(stderr, "Lookup failed\n");
+            break;
+        }
+        for (int i = 0; i < HFV_BR_COUNTERS; ++i) {
+            rb[i] = (double)(b[i] - pb[i]) / dt;
+            rp[i] = (double)(p[i] - pp[i]) / dt;
+        }
+        print_stats(b, p, rb, rp);
+    }
+    return EXIT_SUCCESS;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc >= 2 && strcmp(argv[1], "watch") == 0) return watch(argc - 2, argv + 2);
     if (argc >= 3 && strcmp(argv[1], "key") == 0) {
         if (strcmp(argv[2], "add") == 0) return add_key(argc - 3, argv + 3);
         if (strcmp(argv[2], "remove") == 0) return remove_key(argc - 3, argv + 3);

@@ -77,6 +77,9 @@ def lib():
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_br_process_host": (i32, [vp, vp, sz, vp, vp, sz, sz, vp, vp, vp, vp]),
         "hfv_host_register": (i32, [vp, vp, sz]),
+        "hfv_statsmap_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
+        "hfv_statsmap_add": (i32, [ctypes.c_char_p, vp]),
+        "hfv_statsmap_read": (i32, [ctypes.c_char_p, vp]),
         "hfv_host_unregister": (i32, [vp, vp]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
@@ -433,6 +436,27 @@ def keymap_read(path: str):
 
 
 # ---- batch sharding across GPUs ------------------------------------------------
+
+def statsmap_path(br: str) -> str:
+    buf = ctypes.create_string_buffer(4096)
+    _check(lib().hfv_statsmap_path(br.encode(), buf, 4096))
+    return buf.value.decode()
+
+
+def statsmap_add(path: str, stats):
+    """Add a [64, 2, 11] u64 counter block (hfv_br_process stats) to the pinned stats map."""
+    import numpy as np
+    a = np.ascontiguousarray(np.asarray(stats.cpu().numpy() if hasattr(stats, "cpu") else stats).view(np.uint64))
+    assert a.size == BR_STATS_IFINDEX * 2 * BR_COUNTERS
+    _check(lib().hfv_statsmap_add(path.encode(), a.ctypes.data))
+
+
+def statsmap_read(path: str):
+    import numpy as np
+    a = np.zeros((BR_STATS_IFINDEX, 2, BR_COUNTERS), dtype=np.uint64)
+    _check(lib().hfv_statsmap_read(path.encode(), a.ctypes.data))
+    return a
+
 
 def shard_range(n, world, rank):
     """Contiguous slice of n packets for `rank`, cut on 64-packet boundaries so each rank's

@@ -61,3 +61,28 @@ def test_cli_matches_br_loader_semantics(pin_dir):
     assert bad.returncode != 0 and "Invalid MAC verification key" in bad.stderr
     bad = run("key", env=env)
     assert bad.returncode != 0 and "Usage" in bad.stderr
+
+
+def test_statsmap_and_watch(pin_dir):
+    """Pinned port_stats_map + `hfv-loader watch <br> <iface>` (br_loader.cpp:162-180,
+    stats.cpp:80-144): counters add up across writers; watch prints the stats.cpp table."""
+    import numpy as np
+    path = hfv.statsmap_path("br1-ff00_0_1-1")
+    assert path.startswith(str(pin_dir)) and path.endswith("br1-ff00_0_1-1/port_stats_map")
+    st = np.zeros((64, 2, 11), dtype=np.uint64)
+    st[1, 0, 1], st[1, 1, 1] = 138 * 10, 10
+    st[1, 0, 10], st[1, 1, 10] = 138, 1
+    hfv.statsmap_add(path, st)
+    hfv.statsmap_add(path, st)
+    got = hfv.statsmap_read(path)
+    assert (got == 2 * st).all()
+    r = run("watch", "br1-ff00_0_1-1", "1", "1")
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert len(lines) == 24 and lines[0] == "Verdict             Packets    pkts/s         Bytes    Mbit/s"
+    assert lines[2] == "Forwarded               20          0          2760         0"
+    assert lines[11] == "Invalid HF               2          0           276         0"
+    r = run("watch", "no-such-br", "1", "1")
+    assert r.returncode == 1 and "Lookup failed" in r.stderr
+    with pytest.raises(hfv.HfvError):
+        hfv.statsmap_read(str(pin_dir / "missing" / "port_stats_map"))

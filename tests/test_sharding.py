@@ -57,3 +57,49 @@ def test_two_rank_shards_concatenate(n, keysel):
     hk, valid = orc.key_table(raw)
     full = orc.verify_records(orc.gen_records(n, hk, keysel), hk, valid, keysel)
     assert np.array_equal(got, full)
+
+
+def _br_worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import br_fuzz as F
+    import br_topo as T
+    mac = lambda k, m: orc.cmac(m, k)   # noqa: E731
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    frames, lens, ifidx = F.fuzz_batch(F.hop_inputs(brs, False, mac), "br1", False, n, seed=77, slot=256)
+    a, b = hfv.shard_range(n, world, rank)
+    act, ver, egr, st = brs["br1"].process(frames[a:b].copy(), lens[a:b], ifidx[a:b])   # this rank's frames
+    out = torch.zeros((n, 6), dtype=torch.int64)
+    out[a:b, 0], out[a:b, 1], out[a:b, 2] = torch.from_numpy(act.astype(np.int64)), \
+        torch.from_numpy(ver.astype(np.int64)), torch.from_numpy(egr.astype(np.int64))
+    stats = torch.from_numpy(st.view(np.int64).copy())
+    dist.all_reduce(out)        # disjoint slices
+    dist.all_reduce(stats)      # per-GPU verdict counters merge by summation (like per-CPU maps)
+    if rank == 0:
+        q.put((out.numpy().copy(), stats.numpy().view(np.uint64).copy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_router_shards():
+    """Config 4 sharded over 2 ranks: per-frame results concatenate and the verdict counters
+    of the ranks sum to the single-device counters."""
+    import br_fuzz as F
+    import br_topo as T
+    n = 3001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_br_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out, stats = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mac = lambda k, m: orc.cmac(m, k)   # noqa: E731
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    frames, lens, ifidx = F.fuzz_batch(F.hop_inputs(brs, False, mac), "br1", False, n, seed=77, slot=256)
+    act, ver, egr, st = brs["br1"].process(frames, lens, ifidx)
+    assert (out[:, 0] == act).all() and (out[:, 1] == ver).all() and (out[:, 2] == egr).all()
+    assert (stats == st).all()

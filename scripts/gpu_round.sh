@@ -19,7 +19,9 @@ step() {   # step <name> <timeout-s> <cmd...>
 MODE=${1:-all}
 if [[ $MODE == all || $MODE == test ]]; then
     step pytest_gpu 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-    rc=$?; [[ $rc -gt 1 ]] && exit $rc
+    rc=$?
+    # 1 = some test failed (read the log); anything else non-zero = crash/timeout: stop here
+    if [[ $rc -gt 1 ]]; then exit $rc; fi
 fi
 if [[ $MODE == sweep ]]; then
     step sweep 600 python scripts/sweep.py ${SWEEP_ARGS:-} || exit $?
@@ -41,3 +43,4 @@ if [[ $MODE == all || $MODE == prof || $MODE == br ]]; then
     step rocprof_br 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_br -o run -- \
         python3 bench.py --workload br --cpu-budget 0 || exit $?
 fi
+exit 0

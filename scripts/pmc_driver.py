@@ -12,8 +12,34 @@ import scion_hfv as hfv  # noqa: E402
 from bench import KEY_1111, SEED_RECORDS, key_table_256  # noqa: E402
 
 
+def run_br(reps, n=1 << 20):
+    """Config 4: the bench frame mix through hfv_br_process, reps launches on fresh copies."""
+    from bench import BR_SLOT, br_batch
+    from scion_hfv import topology as TP
+    torch.cuda.set_device(0)
+    ctx = hfv.Ctx(0)
+    ctx.key_add(0, TP.KEYS[1])
+    ctx.br_set_config(TP.br_config("br1"))
+    tmpl, tid, lens, ifidx, _ = br_batch(n, 0)
+    master = torch.from_numpy(tmpl).cuda()[torch.from_numpy(tid.astype("int64")).cuda()]
+    d_len = torch.from_numpy(lens.view("int16")).cuda()
+    d_if = torch.from_numpy(ifidx.view("int32")).cuda()
+    act = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    ver = torch.zeros_like(act)
+    egr = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
+    work = torch.empty_like(master)
+    for _ in range(reps + 1):
+        work.copy_(master)
+        ctx.br_process(work, BR_SLOT, d_len, d_if, n, act, ver, egr, st)
+    torch.cuda.synchronize()
+    ctx.close()
+
+
 def main():
     keysel = sys.argv[1] if len(sys.argv) > 1 else "zero"
+    if keysel == "br":
+        return run_br(int(sys.argv[2]) if len(sys.argv) > 2 else 10)
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
     torch.cuda.set_device(0)

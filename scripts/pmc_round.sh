@@ -14,6 +14,8 @@ groups=(
   "FETCH_SIZE"
   "WRITE_SIZE"
   "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum"
+  "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_REQ_sum"
+  "TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TA_FLAT_WRITE_WAVEFRONTS_sum"
 )
 i=0
 for g in "${groups[@]}"; do
@@ -22,4 +24,8 @@ for g in "${groups[@]}"; do
   timeout -k 10 300 rocprofv3 --pmc $g --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
       python3 scripts/pmc_driver.py $KS 10 > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 scripts/pmc_summary.py $OUT
+if [[ $KS == br ]]; then
+    python3 scripts/pmc_summary.py $OUT 1048576 k_br_process
+else
+    python3 scripts/pmc_summary.py $OUT
+fi

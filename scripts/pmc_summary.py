@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 
-def main(d, sizes):
+def main(d, sizes, kernel="k_verify_records"):
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         disp = defaultdict(lambda: {"name": "", "c": defaultdict(float)})
@@ -20,13 +20,15 @@ def main(d, sizes):
             e["name"] = r["Kernel_Name"]
             e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
         group, first = -1, False
+        if kernel != "k_verify_records":   # one batch size: every launch of `kernel` but the first
+            group, first = 0, True
         for did in sorted(disp):
             e = disp[did]
             if "k_gen_records" in e["name"]:
                 group += 1
                 first = True
                 continue
-            if "k_verify_records" not in e["name"] or group < 0:
+            if kernel not in e["name"] or group < 0:
                 continue
             if first:
                 first = False
@@ -49,4 +51,5 @@ def main(d, sizes):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1048576,16777216").split(",")])
+    main(sys.argv[1], [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1048576,16777216").split(",")],
+         sys.argv[3] if len(sys.argv) > 3 else "k_verify_records")

@@ -57,7 +57,11 @@ def test_fuzz_parity_no_key_and_foreign_key(gpu_ctx):
     hops = F.hop_inputs(brs, False, MAC)
     frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 4000, seed=7)
     v = _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), None)
-    assert hfv.VERDICT["SCION_FORWARD"] not in v
+    # no key: every frame that reaches a hop-field check fails it; internal -> internal IP
+    # forwarding checks none and still forwards (fib_ip_forward path, xdp.c:235-238)
+    assert hfv.VERDICT["INVALID_HF"] in v
+    fwd = np.nonzero(v == hfv.VERDICT["SCION_FORWARD"])[0]
+    assert (ifidx[fwd] == 5).all()
     _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[5])
 
 

@@ -21,6 +21,7 @@
 // key in SGPRs, conflict-free replicated T-tables).
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <stdlib.h>
 
 #include "hfv_aes_dev.h"
 #include "hfv_internal.h"
@@ -29,6 +30,14 @@ namespace hfv {
 
 static __shared__ DevBrConfig s_br;
 static __shared__ unsigned long long s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+
+// Header staging (WIN > 0 kernels): the first kBrWin bytes of each frame of a wave's 64-frame
+// tile, one row of kBrWin / 4 + 1 dwords per frame (the odd row pitch keeps both the staging
+// writes and the per-lane reads bank-conflict free), for up to kBrStageWaves waves per block.
+constexpr int kBrWin = 128;
+constexpr int kBrRow = kBrWin / 4 + 1;
+constexpr int kBrStageWaves = 8;
+static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 
 // enum xdp_action and enum verdict (br/src/bpf/common.h:38-70)
 enum : uint32_t { A_ABORTED = 0, A_DROP = 1, A_PASS = 2, A_TX = 3, A_REDIRECT = 4 };
@@ -58,6 +67,8 @@ __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(
 // Per-frame state: struct headers + the per-CPU scratchpad (common.h:154-225), zeroed per frame.
 struct BrFrame {
     uint8_t *p;
+    uint32_t row;      // dword index of this frame's staged header row in s_hdr
+    int win;           // staged bytes (0: read everything from HBM)
     int len;
     int lim;           // bytes of the frame present in the buffer (min(len, window))
     bool cut;          // a check failed only because the window ended before len
@@ -81,6 +92,31 @@ struct BrFrame {
     uint32_t mi[4];
     uint32_t mac_lo, mac_hi;
 };
+
+// Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
+// staged window come from LDS (a 32-bit field = two aligned ds_read_b32 + v_alignbyte), the
+// rest from the frame in HBM.
+__device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
+{
+    const uint32_t *row = s_hdr + k.row;
+    int a = off >> 2;
+    return __builtin_amdgcn_alignbyte(row[a + 1], row[a], (uint32_t)(off & 3));
+}
+__device__ __forceinline__ uint32_t rd8(const BrFrame &k, int off)
+{
+    if (off < k.win) return reinterpret_cast<const uint8_t *>(s_hdr + k.row)[off];
+    return g8(k.p + off);
+}
+__device__ __forceinline__ uint32_t rd16(const BrFrame &k, int off)
+{
+    if (off + 2 <= k.win) return lds_u32_at(k, off) & 0xffffu;
+    return g16(k.p + off);
+}
+__device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
+{
+    if (off + 4 <= k.win) return lds_u32_at(k, off);
+    return g32(k.p + off);
+}
 
 // Bounds check of the BPF code ("data + n > data_end").  With a header window smaller than the
 // frame, running past the window marks the frame `cut` (the host path re-runs it whole).
@@ -113,48 +149,46 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
     k.verdict = V_NOT_SCION;
     int off = 14;
     if (beyond(k, off)) return -1;
-    uint32_t proto = g16(k.p + 12);
+    uint32_t proto = rd16(k, 12);
     if (proto == 0x0008u) {   // ETH_P_IP, network order
         k.ip = off;
         off += 20;
         if (beyond(k, off)) return -1;
-        const uint8_t *ip = k.p + k.ip;
         k.family = HFV_AF_INET;
-        k.v4_dst = g32(ip + 16);
+        k.v4_dst = rd32(k, k.ip + 16);
         k.ip_residual -= k.v4_dst;
-        k.v4_src = g32(ip + 12);
+        k.v4_src = rd32(k, k.ip + 12);
         k.ip_residual -= k.v4_src;
         k.udp_residual = k.ip_residual;
-        k.v4_ttl = g8(ip + 8);
+        k.v4_ttl = rd8(k, k.ip + 8);
         k.ip_residual -= k.v4_ttl;
-        int skip = 4 * (int)(g8(ip) & 0x0fu) - 20;
+        int skip = 4 * (int)(rd8(k, k.ip) & 0x0fu) - 20;
         if (skip < 0 || skip > 40) return -1;
         off += skip;
-        if (g8(ip + 9) != 17u) return -1;
+        if (rd8(k, k.ip + 9) != 17u) return -1;
     } else if (proto == 0xdd86u) {   // ETH_P_IPV6
         k.ip = off;
         off += 40;
         if (beyond(k, off)) return -1;
-        const uint8_t *ip = k.p + k.ip;
         k.family = HFV_AF_INET6;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            k.v6_dst[i] = g32(ip + 24 + 4 * i);
+            k.v6_dst[i] = rd32(k, k.ip + 24 + 4 * i);
             k.udp_residual -= k.v6_dst[i];
-            k.v6_src[i] = g32(ip + 8 + 4 * i);
+            k.v6_src[i] = rd32(k, k.ip + 8 + 4 * i);
             k.udp_residual -= k.v6_src[i];
         }
-        k.v6_hop = g8(ip + 7);
-        if (g8(ip + 6) != 17u) return -1;
+        k.v6_hop = rd8(k, k.ip + 7);
+        if (rd8(k, k.ip + 6) != 17u) return -1;
     } else {
         return -1;
     }
     k.udp = off;
     off += 8;
     if (beyond(k, off)) return -1;
-    k.udp_dst = g16(k.p + k.udp + 2);
+    k.udp_dst = rd16(k, k.udp + 2);
     k.udp_residual -= k.udp_dst;
-    k.udp_src = g16(k.p + k.udp);
+    k.udp_src = rd16(k, k.udp);
     k.udp_residual -= k.udp_src;
     return off;
 }
@@ -165,7 +199,7 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     k.meta = off;
     off += 4;
     if (beyond(k, off)) return -1;
-    uint32_t raw = g32(k.p + k.meta);
+    uint32_t raw = rd32(k, k.meta);
     k.udp_residual -= raw;
     k.h_meta = sw32(raw);
     k.seg0 = (k.h_meta >> 12) & 0x3fu;
@@ -177,12 +211,12 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     int inf = off + (int)k.curr_inf * 8;
     k.inf = inf;
     if (beyond(k, inf + 8)) return -1;
-    k.seg_id0 = g16(k.p + inf + 2);
+    k.seg_id0 = rd16(k, inf + 2);
     k.udp_residual -= k.seg_id0;
     if (k.curr_inf + 1 < k.num_inf) {
         inf += 8;
         if (beyond(k, inf + 8)) return -1;
-        k.seg_id1 = g16(k.p + inf + 2);
+        k.seg_id1 = rd16(k, inf + 2);
     }
     k.hf = off + (int)k.num_inf * 8 + (int)k.curr_hf * 12;
     if (beyond(k, k.hf + 12)) return -1;
@@ -195,43 +229,42 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
     int sc = off;
     off += 28;
     if (beyond(k, off)) return -1;
-    if ((g8(k.p + sc) >> 4) != 0) {
+    if ((rd8(k, sc) >> 4) != 0) {
         k.verdict = V_NOT_IMPLEMENTED;
         return -1;
     }
-    uint32_t haddr = g8(k.p + sc + 9);
+    uint32_t haddr = rd8(k, sc + 9);
     off += 8 + 4 * (int)((haddr >> 2) & 0x2u) + 4 * (int)((haddr >> 6) & 0x2u);   // SC_GET_DL/SL, scion.h:49-52
     if (beyond(k, off)) return -1;
-    k.path_type = g8(k.p + sc + 8);
+    k.path_type = rd8(k, sc + 8);
     if (k.path_type == 1u) return parse_scion_path(k, off);
     k.verdict = V_NOT_IMPLEMENTED;
     return -1;
 }
 
 // ---- path_processing.h ---------------------------------------------------------------------
-__device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return g8(k.p + inf) & 1u; }
+__device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return rd8(k, inf) & 1u; }
 
 __device__ __forceinline__ void defer_verify(BrFrame &k, int inf, int hf, uint32_t beta_nbo)
 {
     k.need_mac = true;
     k.mi[0] = (beta_nbo & 0xffffu) << 16;
-    k.mi[1] = g32(k.p + inf + 4);
-    k.mi[2] = (g8(k.p + hf + 1) << 8) | (g16(k.p + hf + 2) << 16);
-    k.mi[3] = g16(k.p + hf + 4);
-    k.mac_lo = g32(k.p + hf + 6);
-    k.mac_hi = g16(k.p + hf + 10);
+    k.mi[1] = rd32(k, inf + 4);
+    k.mi[2] = (rd8(k, hf + 1) << 8) | (rd16(k, hf + 2) << 16);
+    k.mi[3] = rd16(k, hf + 4);
+    k.mac_lo = rd32(k, hf + 6);
+    k.mac_hi = rd16(k, hf + 10);
 }
 
 __device__ __forceinline__ bool as_ingress(BrFrame &k)
 {
-    const uint8_t *hf = k.p + k.hf;
-    if (g8(hf) & 0x03u) {
+    if (rd8(k, k.hf) & 0x03u) {
         k.verdict = V_ROUTER_ALERT;
         return false;
     }
     uint32_t c = cons_at(k, k.inf);
     uint32_t beta = sw16(k.seg_id0);
-    if (!c) beta ^= g8(hf + 7) | (g8(hf + 6) << 8);
+    if (!c) beta ^= rd8(k, k.hf + 7) | (rd8(k, k.hf + 6) << 8);
     defer_verify(k, k.inf, k.hf, sw16(beta));
     if (!c) k.seg_id0 = sw16(beta);
     uint32_t seg_end = k.seg0;   // path_processing.h:84-86 adds seg0 for every index
@@ -258,8 +291,7 @@ __device__ __forceinline__ bool as_ingress(BrFrame &k)
 __device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
 {
     k.verdict = A_ABORTED;
-    const uint8_t *hf = k.p + k.hf;
-    if (g8(hf) & 0x03u) {
+    if (rd8(k, k.hf) & 0x03u) {
         k.verdict = V_ROUTER_ALERT;
         return false;
     }
@@ -271,7 +303,7 @@ __device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
     uint32_t beta = sw16(k.segment_switch ? k.seg_id1 : k.seg_id0);
     if (as_ing_ifid == 0) defer_verify(k, k.inf, k.hf, sw16(beta));   // original INF, path_processing.h:142
     if (cons_at(k, inf)) {
-        uint32_t nb = sw16((beta ^ (g8(hf + 7) | (g8(hf + 6) << 8))) & 0xffffu);
+        uint32_t nb = sw16((beta ^ (rd8(k, k.hf + 7) | (rd8(k, k.hf + 6) << 8))) & 0xffffu);
         if (k.segment_switch) k.seg_id1 = nb;
         else k.seg_id0 = nb;
     }
@@ -404,7 +436,7 @@ __device__ __forceinline__ int fib_ip_forward(BrFrame &k)
 {
     uint32_t dst[4];
     if (k.family == HFV_AF_INET) {
-        dst[0] = sw32(g32(k.p + k.ip + 16));   // hdr->ip.v4->daddr
+        dst[0] = sw32(rd32(k, k.ip + 16));   // hdr->ip.v4->daddr
         dst[1] = dst[2] = dst[3] = 0;
     } else {
 #pragma unroll
@@ -440,7 +472,7 @@ __device__ __forceinline__ void rewrite(BrFrame &k)
         k.udp_residual += c;
         ip[8] = (uint8_t)k.v4_ttl;
         k.ip_residual += k.v4_ttl;
-        uint64_t cs = ~(uint64_t)g16(ip + 10) + k.ip_residual + 1;
+        uint64_t cs = ~(uint64_t)rd16(k, k.ip + 10) + k.ip_residual + 1;
         p16(ip + 10, fold_checksum(cs));
     } else {
         uint8_t *ip = p + k.ip;
@@ -470,12 +502,12 @@ __device__ __forceinline__ void rewrite(BrFrame &k)
     if (k.segment_switch) {
         inf += 8;
         if (inf + 8 <= k.len) {
-            k.udp_residual -= g16(p + inf + 2);
+            k.udp_residual -= rd16(k, inf + 2);
             k.udp_residual += k.seg_id1;
             p16(p + inf + 2, k.seg_id1);
         }
     }
-    uint64_t cs = ~(uint64_t)g16(udp + 6) + k.udp_residual + 1;
+    uint64_t cs = ~(uint64_t)rd16(k, k.udp + 6) + k.udp_residual + 1;
     p16(udp + 6, fold_checksum(cs));
 }
 
@@ -496,8 +528,7 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
         int e = ingress_lookup(k);
         if (e < 0) return (int)record<STATS>(k, V_NO_INTERFACE);
         as_ing_ifid = s_br.ingress[e].ifid;
-        const uint8_t *hf = k.p + k.hf;
-        uint32_t hf_ing = cons_at(k, k.inf) ? g16(hf + 2) : g16(hf + 4);
+        uint32_t hf_ing = cons_at(k, k.inf) ? rd16(k, k.hf + 2) : rd16(k, k.hf + 4);
         if (sw16(hf_ing) != as_ing_ifid) return (int)record<STATS>(k, V_NO_INTERFACE);
     }
     if (as_ing_ifid != 0)   // path_type == SCION after parse_scion
@@ -508,8 +539,7 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
         inf += 8;
         if (beyond(k, inf + 8)) return 0;
     }
-    const uint8_t *hf = k.p + k.hf;
-    uint32_t key = sw16(cons_at(k, inf) ? g16(hf + 4) : g16(hf + 2));
+    uint32_t key = sw16(cons_at(k, inf) ? rd16(k, k.hf + 4) : rd16(k, k.hf + 2));
     int f = egress_lookup(key);
     if (f < 0) return (int)record<STATS>(k, V_ABORT);
     const DevBrEgress &fwd = s_br.egress[f];
@@ -538,7 +568,41 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 }
 
 // ---- kernel ------------------------------------------------------------------------------------
-template <int BLOCK, bool STATS>
+template <bool STATS>
+__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const UniformKey &ukey, const Lane &l,
+                                         uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
+                                         int32_t *__restrict__ egress)
+{
+    int a = process_packet<STATS>(k);
+    if (k.cut) {   // headers reach past the window: untouched, uncounted, caller re-runs it whole
+        action[i] = HFV_BR_ACTION_RETRY;
+        verdict[i] = 0;
+        egress[i] = -1;
+        return;
+    }
+    if (a <= 0) {
+        // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
+        uint32_t v = A_ABORTED;
+        bool ok = true;
+        if (k.need_mac) {
+            uint32_t t0, t1;
+            cmac48_macinput<2>(k.mi, ukey, l, t0, t1);
+            ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
+        }
+        if (!ok) v = V_INVALID_HF;
+        else if (tx_port(k.egress_ifindex)) v = V_FORWARD;
+        a = (int)record<STATS>(k, v);
+    }
+    action[i] = (uint8_t)a;
+    verdict[i] = (uint8_t)k.last_verdict;
+    egress[i] = k.egress_ifindex;
+}
+
+// One wave = one tile of 64 consecutive frames (lane = frame).  WIN > 0: the tile's first WIN
+// header bytes per frame are fetched with coalesced 16-byte loads (WIN / 16 frames' chunks per
+// wave instruction... 64 / (WIN / 16) frames per instruction), staged in LDS and parsed from
+// there, and the next tile's bytes are already in flight while this one is parsed.
+template <int BLOCK, bool STATS, int WIN>
 __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st,
                                                       const uint32_t *__restrict__ ttab_img, uint8_t *pkts,
                                                       uint64_t slot, uint32_t maxlen, uint32_t window,
@@ -548,6 +612,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
                                                       int32_t *__restrict__ egress,
                                                       unsigned long long *__restrict__ stats)
 {
+    static_assert(WIN == 0 || (WIN == kBrWin && BLOCK / 64 <= kBrStageWaves), "staging geometry");
+    constexpr int C = WIN > 0 ? WIN / 16 : 1;   // 16-byte chunks per frame
     fill_ttab_dma<2>(ttab_img);
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(&st->br);
@@ -560,37 +626,51 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     __syncthreads();
     const Lane l = lane_bases();
 
-    const uint64_t step = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += step) {
-        BrFrame k = {};
-        k.p = pkts + i * slot;
-        uint32_t len = lens[i];
-        k.len = (int)(len <= maxlen ? len : maxlen);
-        k.lim = k.len < (int)window ? k.len : (int)window;
-        k.ifindex = ifidx[i];
-        int a = process_packet<STATS>(k);
-        if (k.cut) {   // headers reach past the window: untouched, uncounted, caller re-runs it whole
-            action[i] = HFV_BR_ACTION_RETRY;
-            verdict[i] = 0;
-            egress[i] = -1;
-            continue;
+    const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    const uint64_t ntiles = (n + 63) / 64, nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
+    uint64_t t = (uint64_t)blockIdx.x * (BLOCK / 64) + wib;
+    const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
+    uint4 pre[C];
+    auto fetch = [&](uint64_t tt) {
+#pragma unroll
+        for (int r = 0; r < C; ++r) {
+            uint64_t fi = tt * 64 + (uint64_t)(r * (64 / C)) + fr_of;
+            if (fi >= n) fi = n - 1;   // unconditional (counted vmcnt); masked at use
+            pre[r] = *reinterpret_cast<const uint4 *>(pkts + fi * slot + 16 * ch);
         }
-        if (a <= 0) {
-            // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
-            uint32_t v = A_ABORTED;
-            bool ok = true;
-            if (k.need_mac) {
-                uint32_t t0, t1;
-                cmac48_macinput<2>(k.mi, ukey, l, t0, t1);
-                ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
+    };
+    if constexpr (WIN > 0)
+        if (t < ntiles) fetch(t);
+    for (; t < ntiles; t += nwaves) {
+        if constexpr (WIN > 0) {
+            uint32_t *rows = s_hdr + wib * 64 * kBrRow;
+#pragma unroll
+            for (int r = 0; r < C; ++r) {
+                uint32_t *d = rows + (r * (64 / C) + fr_of) * kBrRow + 4 * ch;
+                d[0] = pre[r].x; d[1] = pre[r].y; d[2] = pre[r].z; d[3] = pre[r].w;
             }
-            if (!ok) v = V_INVALID_HF;
-            else if (tx_port(k.egress_ifindex)) v = V_FORWARD;
-            a = (int)record<STATS>(k, v);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (t + nwaves < ntiles) fetch(t + nwaves);
         }
-        action[i] = (uint8_t)a;
-        verdict[i] = (uint8_t)k.last_verdict;
-        egress[i] = k.egress_ifindex;
+        uint64_t i = t * 64 + lane;
+        if (i < n) {
+            BrFrame k = {};
+            k.p = pkts + i * slot;
+            k.win = WIN;
+            k.row = (wib * 64 + lane) * kBrRow;
+            uint32_t len = lens[i];
+            k.len = (int)(len <= maxlen ? len : maxlen);
+            k.lim = k.len < (int)window ? k.len : (int)window;
+            k.ifindex = ifidx[i];
+            br_frame<STATS>(k, i, ukey, l, action, verdict, egress);
+        }
+        if constexpr (WIN > 0) {   // every lane is done with the rows before they are restaged
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
     }
     if constexpr (STATS) {
         __syncthreads();
@@ -601,20 +681,33 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     }
 }
 
-constexpr int kBrBlock = 1024;
-
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
                       void *ev_start, void *ev_stop)
 {
-    uint64_t blocks = (n + kBrBlock - 1) / kBrBlock;
-    uint64_t cap = (uint64_t)g.num_cus;   // one 1024-thread block per CU (LDS: tables + counters)
+    // Staged variant when the 16-byte header loads are aligned and in bounds (HFV_BR_STAGE=0
+    // forces the direct one).  Persistent grid: one block per CU (LDS: tables + counters
+    // [+ header rows]).
+    static const int stage_env = getenv("HFV_BR_STAGE") ? atoi(getenv("HFV_BR_STAGE")) : 1;
+    bool staged = stage_env && slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0;
+    using K = void (*)(const DevState *, const uint32_t *, uint8_t *, uint64_t, uint32_t, uint32_t, const uint16_t *,
+                       const uint32_t *, uint64_t, uint8_t *, uint8_t *, int32_t *, unsigned long long *);
+    K k;
+    int block;
+    if (staged) {
+        block = 512;
+        k = stats ? k_br_process<512, true, kBrWin> : k_br_process<512, false, kBrWin>;
+    } else {
+        block = 1024;
+        k = stats ? k_br_process<1024, true, 0> : k_br_process<1024, false, 0>;
+    }
+    uint64_t blocks = (n + block - 1) / block;
+    uint64_t cap = (uint64_t)g.num_cus;
     unsigned grid = (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
-    auto k = stats ? k_br_process<kBrBlock, true> : k_br_process<kBrBlock, false>;
-    hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBrBlock), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, maxlen, window, len,
-                          ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, maxlen,
+                          window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
                           (unsigned long long *)stats);
     return (int)hipGetLastError();
 }

@@ -155,3 +155,11 @@ def test_host_path_pageable_and_args(gpu_ctx):
     for bad in (60, 1024, 100):
         with pytest.raises(hfv.HfvError):
             gpu_ctx.br_process_host(frames, 512, lens, ifidx, 3000, a, v, e, None, window=bad)
+
+
+def test_fuzz_parity_unstaged_slot(gpu_ctx):
+    """slot % 16 != 0 selects the direct-from-HBM kernel variant (no LDS header staging)."""
+    brs = {b: T.OracleBR(T.br_config(b, True)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, True, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", True, 6000, seed=9, slot=1032, payload_max=1000)
+    _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", True), T.KEYS[1])

@@ -56,11 +56,6 @@ __device__ __forceinline__ uint32_t g32(const uint8_t *q)
 {
     return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
 }
-__device__ __forceinline__ void p16(uint8_t *q, uint32_t v) { q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); }
-__device__ __forceinline__ void p32(uint8_t *q, uint32_t v)
-{
-    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
-}
 __device__ __forceinline__ uint32_t sw16(uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); }
 __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(v); }
 
@@ -68,7 +63,8 @@ __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(
 struct BrFrame {
     uint8_t *p;
     uint32_t row;      // dword index of this frame's staged header row in s_hdr
-    int win;           // staged bytes (0: read everything from HBM)
+    int win;           // staged bytes (0: read and write everything in HBM)
+    bool dirty;        // the staged row was written (write it back at the end of the tile)
     int len;
     int lim;           // bytes of the frame present in the buffer (min(len, window))
     bool cut;          // a check failed only because the window ended before len
@@ -116,6 +112,28 @@ __device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
 {
     if (off + 4 <= k.win) return lds_u32_at(k, off);
     return g32(k.p + off);
+}
+
+// Header writes: bytes inside the staged window go to the LDS row (written back to HBM with
+// coalesced 16-byte stores at the end of the tile), bytes past it straight to HBM.
+__device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
+{
+    if (off < k.win) {
+        reinterpret_cast<uint8_t *>(s_hdr + k.row)[off] = (uint8_t)v;
+        k.dirty = true;
+    } else {
+        k.p[off] = (uint8_t)v;
+    }
+}
+__device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
+{
+    wr8(k, off, v);
+    wr8(k, off + 1, v >> 8);
+}
+__device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
+{
+    wr16(k, off, v);
+    wr16(k, off + 2, v >> 16);
 }
 
 // Bounds check of the BPF code ("data + n > data_end").  With a header window smaller than the
@@ -300,7 +318,9 @@ __device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
         inf += 8;
         if (beyond(k, inf + 8)) return false;
     }
-    uint32_t beta = sw16(k.segment_switch ? k.seg_id1 : k.seg_id0);
+    uint32_t sid = k.seg_id0;
+    if (k.segment_switch) sid = k.seg_id1;
+    uint32_t beta = sw16(sid);
     if (as_ing_ifid == 0) defer_verify(k, k.inf, k.hf, sw16(beta));   // original INF, path_processing.h:142
     if (cons_at(k, inf)) {
         uint32_t nb = sw16((beta ^ (rd8(k, k.hf + 7) | (rd8(k, k.hf + 6) << 8))) & 0xffffu);
@@ -338,15 +358,15 @@ __device__ __forceinline__ int egress_lookup(uint32_t ifid)
 }
 
 // longest-prefix match on (family, destination as big-endian words); ties keep the first entry
-__device__ __forceinline__ int route_lookup(uint32_t family, const uint32_t dst_be[4])
+__device__ __forceinline__ int route_lookup(uint32_t family, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3)
 {
     int best = -1;
     uint32_t best_len = 0;
     for (uint32_t i = 0; i < s_br.n_routes; ++i) {
         const DevBrRoute &r = s_br.routes[i];
         if (r.family != family) continue;
-        uint32_t diff = ((dst_be[0] ^ r.pfx[0]) & r.mask[0]) | ((dst_be[1] ^ r.pfx[1]) & r.mask[1]) |
-                        ((dst_be[2] ^ r.pfx[2]) & r.mask[2]) | ((dst_be[3] ^ r.pfx[3]) & r.mask[3]);
+        uint32_t diff = ((d0 ^ r.pfx[0]) & r.mask[0]) | ((d1 ^ r.pfx[1]) & r.mask[1]) | ((d2 ^ r.pfx[2]) & r.mask[2]) |
+                        ((d3 ^ r.pfx[3]) & r.mask[3]);
         if (diff == 0 && (best < 0 || r.plen > best_len)) {
             best = (int)i;
             best_len = r.plen;
@@ -377,23 +397,33 @@ __device__ __forceinline__ bool fib_result(BrFrame &k, int r)
     return true;
 }
 
+// The family-dependent field updates below are written as selects, not branches: LLVM would
+// otherwise sink the v4 and v6 stores into one store through a pointer phi and keep the
+// frame's address fields in scratch.
+__device__ __forceinline__ void set_dst(BrFrame &k, const uint32_t a[4])
+{
+    const bool v4 = k.family == HFV_AF_INET;
+    k.v4_dst = v4 ? a[0] : k.v4_dst;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k.v6_dst[i] = v4 ? k.v6_dst[i] : a[i];
+}
+__device__ __forceinline__ void set_src(BrFrame &k, const uint32_t a[4])
+{
+    const bool v4 = k.family == HFV_AF_INET;
+    k.v4_src = v4 ? a[0] : k.v4_src;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k.v6_src[i] = v4 ? k.v6_src[i] : a[i];
+    k.v4_ttl = v4 ? 64u : k.v4_ttl;
+    k.v6_hop = v4 ? k.v6_hop : 64u;
+}
+
 __device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link)
 {
     k.udp_dst = link.remote_port;
     k.udp_src = link.local_port;
-    if (k.family == HFV_AF_INET) {
-        k.v4_dst = link.remote[0];
-        k.v4_src = link.local[0];
-        k.v4_ttl = 64;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            k.v6_dst[i] = link.remote[i];
-            k.v6_src[i] = link.local[i];
-        }
-        k.v6_hop = 64;
-    }
-    int r = route_lookup(k.family, link.remote_be);
+    set_dst(k, link.remote);
+    set_src(k, link.local);
+    int r = route_lookup(k.family, link.remote_be[0], link.remote_be[1], link.remote_be[2], link.remote_be[3]);
     if (!fib_result(k, r)) return -1;
     return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
 }
@@ -401,13 +431,8 @@ __device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link
 __device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
 {
     k.udp_dst = sib.remote_port;
-    if (k.family == HFV_AF_INET) {
-        k.v4_dst = sib.remote[0];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) k.v6_dst[i] = sib.remote[i];
-    }
-    int r = route_lookup(k.family, sib.remote_be);
+    set_dst(k, sib.remote);
+    int r = route_lookup(k.family, sib.remote_be[0], sib.remote_be[1], sib.remote_be[2], sib.remote_be[3]);
     if (!fib_result(k, r)) return -1;
     uint32_t out_if = r >= 0 ? s_br.routes[r].ifindex : 0;
     int s = int_iface(out_if);
@@ -421,28 +446,17 @@ __device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
         return -1;
     }
     k.udp_src = src.port;
-    if (k.family == HFV_AF_INET) {
-        k.v4_src = src.addr[0];
-        k.v4_ttl = 64;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) k.v6_src[i] = src.addr[i];
-        k.v6_hop = 64;
-    }
+    set_src(k, src.addr);
     return (int)out_if;
 }
 
 __device__ __forceinline__ int fib_ip_forward(BrFrame &k)
 {
-    uint32_t dst[4];
-    if (k.family == HFV_AF_INET) {
-        dst[0] = sw32(rd32(k, k.ip + 16));   // hdr->ip.v4->daddr
-        dst[1] = dst[2] = dst[3] = 0;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dst[i] = sw32(k.v6_dst[i]);
-    }
-    int r = route_lookup(k.family, dst);
+    int r;
+    if (k.family == HFV_AF_INET)   // hdr->ip.v4->daddr
+        r = route_lookup(k.family, sw32(rd32(k, k.ip + 16)), 0, 0, 0);
+    else
+        r = route_lookup(k.family, sw32(k.v6_dst[0]), sw32(k.v6_dst[1]), sw32(k.v6_dst[2]), sw32(k.v6_dst[3]));
     if (!fib_result(k, r)) return -1;
     k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
     return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
@@ -460,55 +474,51 @@ __device__ __forceinline__ uint32_t fold_checksum(uint64_t c)
 
 __device__ __forceinline__ void rewrite(BrFrame &k)
 {
-    uint8_t *p = k.p;
-    p32(p, k.dmac_lo); p16(p + 4, k.dmac_hi);
-    p32(p + 6, k.smac_lo); p16(p + 10, k.smac_hi);
+    wr32(k, 0, k.dmac_lo); wr16(k, 4, k.dmac_hi);
+    wr32(k, 6, k.smac_lo); wr16(k, 10, k.smac_hi);
     if (k.family == HFV_AF_INET) {
-        uint8_t *ip = p + k.ip;
-        p32(ip + 16, k.v4_dst);
-        p32(ip + 12, k.v4_src);
+        wr32(k, k.ip + 16, k.v4_dst);
+        wr32(k, k.ip + 12, k.v4_src);
         uint64_t c = (uint64_t)k.v4_dst + (uint64_t)k.v4_src;
         k.ip_residual += c;
         k.udp_residual += c;
-        ip[8] = (uint8_t)k.v4_ttl;
+        wr8(k, k.ip + 8, k.v4_ttl);
         k.ip_residual += k.v4_ttl;
         uint64_t cs = ~(uint64_t)rd16(k, k.ip + 10) + k.ip_residual + 1;
-        p16(ip + 10, fold_checksum(cs));
+        wr16(k, k.ip + 10, fold_checksum(cs));
     } else {
-        uint8_t *ip = p + k.ip;
         if (k.ip + 24 + 16 < k.len && k.ip + 8 + 16 < k.len) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                p32(ip + 24 + 4 * i, k.v6_dst[i]);
+                wr32(k, k.ip + 24 + 4 * i, k.v6_dst[i]);
                 k.udp_residual += k.v6_dst[i];
-                p32(ip + 8 + 4 * i, k.v6_src[i]);
+                wr32(k, k.ip + 8 + 4 * i, k.v6_src[i]);
                 k.udp_residual += k.v6_src[i];
             }
         }
-        ip[7] = (uint8_t)k.v6_hop;
+        wr8(k, k.ip + 7, k.v6_hop);
     }
-    uint8_t *udp = p + k.udp;
-    p16(udp + 2, k.udp_dst);
-    p16(udp, k.udp_src);
+    wr16(k, k.udp + 2, k.udp_dst);
+    wr16(k, k.udp, k.udp_src);
     k.udp_residual += k.udp_dst;
     k.udp_residual += k.udp_src;
     // path_type is SCION here (the only type process_packet lets through)
     uint32_t meta = (k.h_meta & 0x00ffffffu) | ((k.curr_hf & 0x3fu) << 24) | (k.curr_inf << 30);
-    p32(p + k.meta, sw32(meta));
+    wr32(k, k.meta, sw32(meta));
     k.udp_residual += sw32(meta);
     int inf = k.inf;
-    p16(p + inf + 2, k.seg_id0);
+    wr16(k, inf + 2, k.seg_id0);
     k.udp_residual += k.seg_id0;
     if (k.segment_switch) {
         inf += 8;
         if (inf + 8 <= k.len) {
             k.udp_residual -= rd16(k, inf + 2);
             k.udp_residual += k.seg_id1;
-            p16(p + inf + 2, k.seg_id1);
+            wr16(k, inf + 2, k.seg_id1);
         }
     }
     uint64_t cs = ~(uint64_t)rd16(k, k.udp + 6) + k.udp_residual + 1;
-    p16(udp + 6, fold_checksum(cs));
+    wr16(k, k.udp + 6, fold_checksum(cs));
 }
 
 // ---- xdp.c: process_packet -----------------------------------------------------------------
@@ -569,7 +579,7 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 
 // ---- kernel ------------------------------------------------------------------------------------
 template <bool STATS>
-__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const UniformKey &ukey, const Lane &l,
+__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTable *keys, const Lane &l,
                                          uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
                                          int32_t *__restrict__ egress)
 {
@@ -585,6 +595,8 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const UniformKe
         uint32_t v = A_ABORTED;
         bool ok = true;
         if (k.need_mac) {
+            // slot-0 key (xdp.c:82) through the scalar cache, only where a hop field is checked
+            const UniformKey ukey(keys);
             uint32_t t0, t1;
             cmac48_macinput<2>(k.mi, ukey, l, t0, t1);
             ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
@@ -622,7 +634,6 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     }
     if constexpr (STATS)
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) s_stats[e] = 0;
-    UniformKey ukey(&st->keys);
     __syncthreads();
     const Lane l = lane_bases();
 
@@ -655,6 +666,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             if (t + nwaves < ntiles) fetch(t + nwaves);
         }
         uint64_t i = t * 64 + lane;
+        bool dirty = false;
         if (i < n) {
             BrFrame k = {};
             k.p = pkts + i * slot;
@@ -664,7 +676,24 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             k.len = (int)(len <= maxlen ? len : maxlen);
             k.lim = k.len < (int)window ? k.len : (int)window;
             k.ifindex = ifidx[i];
-            br_frame<STATS>(k, i, ukey, l, action, verdict, egress);
+            br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
+            dirty = k.dirty;
+        }
+        if constexpr (WIN > 0) {
+            // write the rewritten rows back: 16-byte stores, WIN / 16 lanes per frame
+            uint64_t dmask = __ballot(dirty);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t *rows = s_hdr + wib * 64 * kBrRow;
+#pragma unroll
+            for (int r = 0; r < C; ++r) {
+                uint32_t fr = r * (64 / C) + fr_of;
+                if ((dmask >> fr) & 1u) {
+                    const uint32_t *q = rows + fr * kBrRow + 4 * ch;
+                    *reinterpret_cast<uint4 *>(pkts + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
+                }
+            }
         }
         if constexpr (WIN > 0) {   // every lane is done with the rows before they are restaged
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

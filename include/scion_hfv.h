@@ -247,7 +247,10 @@ int hfv_statsmap_path(const char *br, char *out, size_t len);
 int hfv_statsmap_add(const char *path, const uint64_t *stats);   /* creates the map if needed */
 int hfv_statsmap_read(const char *path, uint64_t *stats);
 
-/* Page-lock an existing host buffer (e.g. the RX ring) for direct DMA by this ctx's GPU. */
+/* Page-lock and map an existing host buffer (e.g. the RX ring) for this ctx's GPU (at most 16
+ * per ctx).  hfv_br_process_host on frames inside a registered buffer runs zero-copy: the
+ * kernel reads the header windows across PCIe itself and writes back only rewritten rows
+ * (`window` is then unused); registered len/ifindex/output arrays are used in place. */
 int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes);
 int hfv_host_unregister(hfv_ctx *ctx, void *ptr);
 

@@ -166,6 +166,16 @@ struct hfv_ctx {
     uint8_t *brh_dio[2] = {nullptr, nullptr};   // len u16 | ifindex u32 | action u8 | verdict u8 | egress i32
     uint8_t *brh_hio[2] = {nullptr, nullptr};   // pinned twin of brh_dio
     uint64_t *brh_dstats = nullptr;
+    // host buffers registered with hfv_host_register (mapped: the kernels can address them)
+    struct HostRange {
+        uint8_t *host;
+        size_t bytes;
+        uint8_t *dev;
+    };
+    HostRange hreg[16] = {};
+    int nhreg = 0;
+    uint8_t *zc_meta = nullptr;   // zero-copy path: device len/ifindex/outputs for unregistered arrays
+    size_t zc_cap = 0;
 };
 
 // NULL is HIP's default stream, as for any HIP API taking a stream.
@@ -306,6 +316,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
     }
     if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
+    if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
     keymap_close(ctx->keymap);
     for (int i = 0; i < 2; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
@@ -410,6 +421,7 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
         if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
     }
     if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
+    if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
     keymap_close(ctx->keymap);
     ctx->keymap = m;
     strcpy(ctx->keymap_path, path);
@@ -732,6 +744,64 @@ static void brh_results(hfv_ctx *ctx, int sl, size_t cnt, uint8_t *action, uint8
     memcpy(egress, hio + kBrChunk * 8, cnt * 4);
 }
 
+// Device address of [p, p + bytes) if it lies in a mapped registered buffer, else NULL.
+static uint8_t *host_dev_ptr(hfv_ctx *ctx, const void *p, size_t bytes)
+{
+    const uint8_t *q = (const uint8_t *)p;
+    for (int i = 0; i < ctx->nhreg; ++i) {
+        const hfv_ctx::HostRange &r = ctx->hreg[i];
+        if (q >= r.host && q + bytes <= r.host + r.bytes) return r.dev + (q - r.host);
+    }
+    return nullptr;
+}
+
+// Zero-copy: the frames are in a registered (mapped) ring, so the kernel reads each header
+// window across PCIe itself and writes back only the rewritten rows; no DMA of frame bytes and
+// no retry pass (the whole frame stays addressable).  Per-frame metadata uses the caller's
+// arrays in place when they are registered too, else one copy each way.
+static int br_zero_copy(hfv_ctx *ctx, uint8_t *dframes, size_t slot, const uint16_t *len, const uint32_t *ifx,
+                        size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress, uint64_t *stats)
+{
+    hipStream_t st = ctx->stream;
+    if (!ctx->brh_dstats) HIP_TRY(hipMalloc((void **)&ctx->brh_dstats, HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8));
+    HIP_TRY(hipMemsetAsync(ctx->brh_dstats, 0, HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8, st));
+    uint16_t *dlen = (uint16_t *)host_dev_ptr(ctx, len, n * 2);
+    uint32_t *difx = (uint32_t *)host_dev_ptr(ctx, ifx, n * 4);
+    uint8_t *dact = host_dev_ptr(ctx, action, n), *dver = host_dev_ptr(ctx, verdict, n);
+    int32_t *degr = (int32_t *)host_dev_ptr(ctx, egress, n * 4);
+    size_t need = n * 16;
+    if ((!dlen || !difx || !dact || !dver || !degr) && ctx->zc_cap < need) {
+        if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
+        ctx->zc_meta = nullptr;
+        HIP_TRY(hipMalloc((void **)&ctx->zc_meta, need));
+        ctx->zc_cap = need;
+    }
+    uint8_t *m = ctx->zc_meta;
+    if (!dlen) { dlen = (uint16_t *)m; HIP_TRY(hipMemcpyAsync(dlen, len, n * 2, hipMemcpyHostToDevice, st)); }
+    if (!difx) { difx = (uint32_t *)(m + n * 4); HIP_TRY(hipMemcpyAsync(difx, ifx, n * 4, hipMemcpyHostToDevice, st)); }
+    bool cp_act = !dact, cp_ver = !dver, cp_egr = !degr;
+    if (cp_act) dact = m + n * 2;
+    if (cp_ver) dver = m + n * 3;
+    if (cp_egr) degr = (int32_t *)(m + n * 8);
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_br_process(ctx->geom, ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
+                              degr, ctx->brh_dstats, st);
+    rc = after_launch(ctx, st, e, "br_process launch");
+    if (rc) return rc;
+    if (cp_act) HIP_TRY(hipMemcpyAsync(action, dact, n, hipMemcpyDeviceToHost, st));
+    if (cp_ver) HIP_TRY(hipMemcpyAsync(verdict, dver, n, hipMemcpyDeviceToHost, st));
+    if (cp_egr) HIP_TRY(hipMemcpyAsync(egress, degr, n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (stats) {
+        uint64_t tmp[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+        HIP_TRY(hipMemcpy(tmp, ctx->brh_dstats, sizeof tmp, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < sizeof tmp / 8; ++k) stats[k] += tmp[k];
+    }
+    return 0;
+}
+
 int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,
                         const uint32_t *ingress_ifindex, size_t n, size_t window, uint8_t *action,
                         uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats)
@@ -743,6 +813,8 @@ int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16
     if (window == 0) window = slot < 256 ? slot : 256;
     if (window < 64 || (window & 7) || window > slot) return fail(-EINVAL, "window must be a multiple of 8 in [64, slot]");
     DeviceGuard g(ctx->device);
+    uint8_t *dframes = host_dev_ptr(ctx, frames, n * slot);
+    if (dframes) return br_zero_copy(ctx, dframes, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex, stats);
     int rc = brh_buffers(ctx, window > slot ? slot : window);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(ctx->brh_dstats, 0, HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8, ctx->hstream[0]));
@@ -811,8 +883,16 @@ int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16
 int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes)
 {
     if (!ctx || !ptr || !bytes) return fail(-EINVAL, "bad argument");
+    if (ctx->nhreg == 16) return fail(-ENOMEM, "at most 16 registered host buffers per ctx");
     DeviceGuard g(ctx->device);
-    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    void *dev = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dev, ptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(ptr);
+        return hip_fail(e, "hipHostGetDevicePointer");
+    }
+    ctx->hreg[ctx->nhreg++] = {(uint8_t *)ptr, bytes, (uint8_t *)dev};
     return 0;
 }
 
@@ -820,8 +900,14 @@ int hfv_host_unregister(hfv_ctx *ctx, void *ptr)
 {
     if (!ctx || !ptr) return fail(-EINVAL, "bad argument");
     DeviceGuard g(ctx->device);
-    HIP_TRY(hipHostUnregister(ptr));
-    return 0;
+    for (int i = 0; i < ctx->nhreg; ++i) {
+        if (ctx->hreg[i].host != ptr) continue;
+        HIP_TRY(hipDeviceSynchronize());   // no launch may still address it
+        HIP_TRY(hipHostUnregister(ptr));
+        ctx->hreg[i] = ctx->hreg[--ctx->nhreg];
+        return 0;
+    }
+    return fail(-EINVAL, "buffer was not registered with this ctx");
 }
 
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two

@@ -32,6 +32,7 @@ fi
 if [[ $MODE == all || $MODE == bench || $MODE == br ]]; then
     step bench_br 600 python bench.py --workload br || exit $?
     step bench_brhost 600 python bench.py --workload br-host || exit $?
+    step bench_brhost_dma 600 python bench.py --workload br-host --no-register || exit $?
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
     # the same command as the bench step, under the kernel tracer

@@ -104,11 +104,13 @@ def test_stats_accumulate_and_bad_args(gpu_ctx):
         gpu_ctx.br_set_config(cfg)
 
 
-@pytest.mark.parametrize("window", [64, 256, 0])
-def test_host_path_matches_oracle(gpu_ctx, window):
-    """Config 5 (hfv_br_process_host): frames in host memory, only a header window crosses
-    PCIe; frames whose headers pass the window (long paths, and for window 64 nearly all) are
-    re-run whole.  Result identical to the oracle on the full frames."""
+@pytest.mark.parametrize("window,register", [(64, False), (256, False), (0, False), (0, True)],
+                         ids=["win64", "win256", "windefault", "zerocopy"])
+def test_host_path_matches_oracle(gpu_ctx, window, register):
+    """Config 5 (hfv_br_process_host): frames in host memory.  Unregistered: only a header
+    window crosses PCIe by DMA; frames whose headers pass the window (long paths, and for
+    window 64 nearly all) are re-run whole.  Registered: zero-copy, the kernel reads the
+    mapped ring itself.  Result identical to the oracle on the full frames either way."""
     brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
     hops = F.hop_inputs(brs, False, MAC)
     frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 70000, seed=21, payload_max=1500)
@@ -128,11 +130,15 @@ def test_host_path_matches_oracle(gpu_ctx, window):
     v = np.zeros(n, np.uint8)
     e = np.zeros(n, np.int32)
     st = np.zeros((64, 2, 11), np.uint64)
-    gpu_ctx.host_register(got)
+    if register:
+        gpu_ctx.host_register(got)
+        gpu_ctx.host_register(a)      # an output array used in place as well
     try:
         gpu_ctx.br_process_host(got, T.SLOT, lens, ifidx, n, a, v, e, st, window=window)
     finally:
-        gpu_ctx.host_unregister(got)
+        if register:
+            gpu_ctx.host_unregister(got)
+            gpu_ctx.host_unregister(a)
     assert (a == oa).all() and (v == ov).all() and (e == oe).all()
     assert (got == ref).all()
     assert (st == os_).all()

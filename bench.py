@@ -327,7 +327,7 @@ def run_br_host(args, rank, world, local):
     ctx.br_set_config(TP.br_config("br1"))
     tmpl, tid, lens, ifidx, n_good = br_batch(n, rank)
     pristine = tmpl[tid]                                   # n x 2 KiB in host memory
-    frames = np.empty_like(pristine)
+    frames = hfv.host_array(pristine.shape, np.uint8)
     if not args.no_register:
         ctx.host_register(frames)   # mapped: zero-copy (the kernel reads header windows over PCIe)
     act = np.zeros(n, np.uint8)

@@ -437,6 +437,17 @@ def keymap_read(path: str):
 
 # ---- batch sharding across GPUs ------------------------------------------------
 
+def host_array(shape, dtype):
+    """Zero-filled numpy array in page-aligned anonymous memory, suitable for Ctx.host_register
+    (an RX ring, or the per-frame metadata arrays of br_process_host)."""
+    import mmap
+    import numpy as np
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    buf = mmap.mmap(-1, max(1, count * dt.itemsize))
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
+
+
 def statsmap_path(br: str) -> str:
     buf = ctypes.create_string_buffer(4096)
     _check(lib().hfv_statsmap_path(br.encode(), buf, 4096))

@@ -125,8 +125,9 @@ def test_host_path_matches_oracle(gpu_ctx, window, register):
     gpu_ctx.br_set_config(T.br_config("br1"))
     gpu_ctx.key_add(0, T.KEYS[1])
     n = len(frames)
-    got = frames.copy()
-    a = np.zeros(n, np.uint8)
+    got = hfv.host_array(frames.shape, np.uint8) if register else frames.copy()
+    got[:] = frames
+    a = hfv.host_array(n, np.uint8) if register else np.zeros(n, np.uint8)
     v = np.zeros(n, np.uint8)
     e = np.zeros(n, np.int32)
     st = np.zeros((64, 2, 11), np.uint64)

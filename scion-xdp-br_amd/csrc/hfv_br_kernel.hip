@@ -127,13 +127,30 @@ __device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
 }
 __device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
 {
-    wr8(k, off, v);
-    wr8(k, off + 1, v >> 8);
+    if (off + 2 <= k.win) {   // whole field in the window (the common case): one check
+        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
+        k.dirty = true;
+    } else if (off >= k.win) {
+        k.p[off] = (uint8_t)v; k.p[off + 1] = (uint8_t)(v >> 8);
+    } else {
+        wr8(k, off, v);
+        wr8(k, off + 1, v >> 8);
+    }
 }
 __device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
 {
-    wr16(k, off, v);
-    wr16(k, off + 2, v >> 16);
+    if (off + 4 <= k.win) {
+        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+        k.dirty = true;
+    } else if (off >= k.win) {
+        uint8_t *q = k.p + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+    } else {
+        wr16(k, off, v);
+        wr16(k, off + 2, v >> 16);
+    }
 }
 
 // Bounds check of the BPF code ("data + n > data_end").  With a header window smaller than the

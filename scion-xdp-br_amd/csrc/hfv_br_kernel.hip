@@ -648,6 +648,22 @@ __device__ __forceinline__ bool br_frame(F &k, uint64_t i, const DevKeyTable *ke
     return true;
 }
 
+// The rare rerun of a frame cut at the staged window, kept out of line so that its register
+// needs do not weigh on the staged parser.
+template <bool STATS>
+__device__ __attribute__((noinline)) void br_frame_hbm(uint8_t *p, int len, int lim, uint32_t ifx, uint64_t i,
+                                                      const DevKeyTable *keys, uint8_t *action, uint8_t *verdict,
+                                                      int32_t *egress)
+{
+    BrFrameT<false> k = {};
+    k.p = p;
+    k.len = len;
+    k.lim = lim;
+    k.ifindex = ifx;
+    const Lane l = lane_bases();
+    br_frame<STATS>(k, i, keys, l, action, verdict, egress);
+}
+
 // One wave = one tile of 64 consecutive frames (lane = frame).  WIN > 0: the tile's first WIN
 // header bytes per frame are fetched with coalesced 16-byte loads (WIN / 16 frames' chunks per
 // wave instruction... 64 / (WIN / 16) frames per instruction), staged in LDS and parsed from
@@ -737,14 +753,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             }
         }
         if constexpr (WIN > 0) {
-            if (defer) {   // rare: headers past the staged window, again straight from HBM
-                BrFrameT<false> k = {};
-                k.p = pkts + i * slot;
-                k.len = flen;
-                k.lim = flim;
-                k.ifindex = ifx;
-                br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
-            }
+            if (defer)   // rare: headers past the staged window, again straight from HBM
+                br_frame_hbm<STATS>(pkts + i * slot, flen, flim, ifx, i, &st->keys, action, verdict, egress);
             // write the rewritten rows back: 16-byte stores, WIN / 16 lanes per frame
             uint64_t dmask = __ballot(dirty);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

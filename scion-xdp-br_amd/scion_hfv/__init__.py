@@ -45,9 +45,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise HfvError(-errno.ENOENT, f"{LIB_PATH} not built (run `make -C {PKG_ROOT}`)")
-    L = ctypes.CDLL(LIB_PATH)
+    path = os.environ.get("HFV_LIB") or LIB_PATH   # HFV_LIB: another build (A/B measurements)
+    if not os.path.exists(path):
+        raise HfvError(-errno.ENOENT, f"{path} not built (run `make -C {PKG_ROOT}`)")
+    L = ctypes.CDLL(path)
     vp, sz, u32, u64, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     sigs = {
         "hfv_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),

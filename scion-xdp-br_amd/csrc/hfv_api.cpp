@@ -541,9 +541,10 @@ int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
     if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");
     const KernelVariant &a = ctx->geom.single, &b = ctx->geom.multi;
     snprintf(buf, len,
-             "zero: block=%d pf=%d tab=%d dma=%d np=%d dyn=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d dma=%d np=%d "
-             "dyn=%d grid=%dx%d",
-             a.block, a.pf, a.tab, a.dma, a.np, a.dyn, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab, b.dma,
+             "zero: block=%d pf=%d tab=%d dma=%d np=%d dyn=%d bs=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d dma=%d "
+             "np=%d dyn=%d grid=%dx%d",
+             a.block, a.pf, a.tab, a.dma, a.np, a.dyn, a.bs, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab,
+             b.dma,
              b.np, b.dyn, ctx->geom.num_cus, b.blocks_per_cu);
     return 0;
 }

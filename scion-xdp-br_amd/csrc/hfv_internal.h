@@ -82,7 +82,10 @@ struct KernelVariant {
     int dma;             // 1: fill the LDS tables from ttab_img by LDS-DMA; 0: compute them
     int np;              // packets per lane computed together (1 or 2)
     int dyn;             // 1: waves pull tiles from a per-block LDS queue; 0: static stride
+    int bs;              // KEYSEL_ZERO only: 0 T-table waves only; 1..4 bitsliced waves per
+                         // block beside the T-table waves (hybrid); kBsOnly all bitsliced
 };
+constexpr int kBsOnly = 99;
 
 struct LaunchGeom {
     int num_cus;

@@ -24,6 +24,7 @@
 #include <hip/hip_ext.h>
 
 #include "hfv_aes_dev.h"
+#include "hfv_bitslice.h"
 #include "hfv_internal.h"
 
 namespace hfv {
@@ -203,6 +204,242 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
             st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                      ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// bitsliced verify (hfv_bitslice.h): VALU-only AES for chunks of 512 records per wave
+// ---------------------------------------------------------------------------------------
+// Per-wave LDS staging of a chunk: 6 words per record (macinput w0..w3, expected MAC words
+// e0 = mac0..3, e1 = mac4..5), quad q's 32 records at dword q * kBsQuadStride + 6 p.  The
+// 4-dword pad per quad makes the transposing reads (lane (q, c) reads word c of record p of
+// quad q, all lanes the same p) bank-conflict free: bank = (4 q + c + 6 p) % 32.
+constexpr uint32_t kBsChunk = 512;                 // records per wave per chunk = 8 tiles
+constexpr uint32_t kBsQuadStride = 32 * 6 + 4;     // dwords
+constexpr uint32_t kBsWaveDwords = 16 * kBsQuadStride;
+constexpr uint32_t kBsMaxWaves = 4;
+static __shared__ uint32_t s_bs[kBsMaxWaves * kBsWaveDwords];   // 49 KiB
+static __shared__ uint32_t s_fill_done;
+
+// AddRoundKey + ShiftRows on the quad: row r of lane c comes from lane (c + r) % 4
+// (DPP quad_perm on the XOR's first operand).
+template <int R>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v)
+{
+    constexpr int ctrl = R == 1 ? 0x39 : R == 2 ? 0x4e : 0x93;   // quad_perm [1230], [2301], [3012]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void bs_ark_sr(uint32_t (&s)[32], uint32_t kk)
+{
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s[b] ^= bs::kmask(kk, b);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s[8 + b] = quad_rot<1>(s[8 + b]) ^ bs::kmask(kk, 8 + b);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s[16 + b] = quad_rot<2>(s[16 + b]) ^ bs::kmask(kk, 16 + b);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s[24 + b] = quad_rot<3>(s[24 + b]) ^ bs::kmask(kk, 24 + b);
+}
+
+// The lane's key column for the ARK+SR step before round r + 1 (r = 0..9): row 0 of the
+// device key image is rk0 ^ K1, rows 1..9 are rot16 of rk1..rk9 (hfv_tables.h).  The row is
+// a wave-uniform scalar load (K$), so the round loop need not be unrolled to keep keys in
+// registers.
+// The four candidate words are formed on the scalar unit; the lane picks its column with
+// per-lane all-ones/all-zeros selectors (sel[k] = -(c == k)), so nothing branches on c.
+struct BsLaneSel {
+    uint32_t sel[4];
+    __device__ __forceinline__ explicit BsLaneSel(uint32_t c)
+    {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sel[k] = vconst(0) - (c == (uint32_t)k ? 1u : 0u);
+    }
+    __device__ __forceinline__ uint32_t pick(const uint32_t (&w)[4]) const
+    {
+        return (w[0] & sel[0]) | (w[1] & sel[1]) | (w[2] & sel[2]) | (w[3] & sel[3]);
+    }
+};
+__device__ __forceinline__ uint32_t bs_round_key(const DevKeyTable *tab, uint32_t r, const BsLaneSel &ls)
+{
+    const uint32_t *p = tab->rows[r][0];
+    uint32_t w[4] = {p[0], p[1], p[2], p[3]};
+    if (r >= 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (w[i] >> 16) | (w[i] << 16);
+    }
+    uint32_t k[4];   // k[c] = the pre-shifted key column of lane c (bs::shifted_key_column)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        k[c] = (w[c] & 0xffu) | (w[(c + 1) & 3] & 0xff00u) | (w[(c + 2) & 3] & 0xff0000u) | (w[(c + 3) & 3] & 0xff000000u);
+    return ls.pick(k);
+}
+// column c of rk10, added after the last SubBytes (no shift)
+__device__ __forceinline__ uint32_t bs_final_key(const DevKeyTable *tab, const BsLaneSel &ls)
+{
+    const uint32_t *p = tab->rows[10][0];
+    const uint32_t w[4] = {p[0], p[1], p[2], p[3]};
+    return ls.pick(w);
+}
+
+// One chunk of up to 512 records [base, base + 512) by one wave: coalesced record loads
+// (8 tiles), macinput + expected words staged in the wave's LDS region, transposed into
+// bit planes per quad, 10 bitsliced rounds, then the 48-bit compare (xdp.c:89-90) in the
+// bitsliced domain: lane 0 of a quad holds tag bytes 0..3 (column 0), lane 1 bytes 4..5.
+// Records >= limit get a 0 bit; words32 = number of 32-bit bitmap words that may be written.
+__device__ __forceinline__ void bs_chunk(const uint8_t *__restrict__ recs, uint64_t stride, uint64_t base,
+                                         uint64_t limit, uint32_t inf_off, uint32_t hf_off, uint32_t *lds,
+                                         const DevKeyTable *__restrict__ tab, uint32_t *__restrict__ bits32, uint64_t words32,
+                                         uint32_t lane)
+{
+    const uint64_t last = limit - 1;
+    RecWords r[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) r[it] = load_rec(recs, stride, base + it * 64 + lane, last, inf_off, hf_off);
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        uint32_t w[4];
+        rec_macinput(r[it], w);
+        uint32_t e0 = __builtin_amdgcn_alignbit(r[it].hfb, r[it].hfa.y, 16), e1 = r[it].hfb >> 16;
+        uint32_t *d = lds + (2 * it + (lane >> 5)) * kBsQuadStride + 6 * (lane & 31);
+        *reinterpret_cast<uint2 *>(d) = make_uint2(w[0], w[1]);
+        *reinterpret_cast<uint2 *>(d + 2) = make_uint2(w[2], w[3]);
+        *reinterpret_cast<uint2 *>(d + 4) = make_uint2(e0, e1);
+    }
+    const uint32_t q = lane >> 2, c = lane & 3;
+    const BsLaneSel ls(c);
+    const uint32_t *src = lds + q * kBsQuadStride + c;
+    uint32_t s[32];
+#pragma unroll
+    for (int p = 0; p < 32; ++p) s[p] = src[6 * p];
+    bs::transpose32(s);
+#pragma unroll 1
+    for (uint32_t rd = 0; rd < 9; ++rd) {
+        bs_ark_sr(s, bs_round_key(tab, rd, ls));
+        bs::sub_bytes(s);
+        bs::mix_columns(s);
+    }
+    bs_ark_sr(s, bs_round_key(tab, 9, ls));
+    bs::sub_bytes(s);
+    const uint32_t k10 = bs_final_key(tab, ls);
+    uint32_t e[32];
+    const uint32_t *es = lds + q * kBsQuadStride + 4 + (c & 1);
+#pragma unroll
+    for (int p = 0; p < 32; ++p) e[p] = es[6 * p];
+    bs::transpose32(e);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lo |= HFV_BOP3(s[i], e[i], bs::kmask(k10, i), 0x96);
+#pragma unroll
+    for (int i = 16; i < 32; ++i) hi |= HFV_BOP3(s[i], e[i], bs::kmask(k10, i), 0x96);
+    uint32_t m = lo | (c == 0 ? hi : 0u);
+    m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x55, 0xf, 0xf, false);   // quad_perm [1111]: + lane 1
+    const uint64_t first = base + 32 * q;
+    uint32_t valid = first >= limit ? 0u : (limit - first >= 32 ? ~0u : ((1u << (limit - first)) - 1u));
+    const uint64_t word = base / 32 + q;
+    if (c == 0 && word < words32) bits32[word] = ~m & valid;
+}
+
+// Pure bitsliced verify (KEYSEL_ZERO): every wave works through 512-record chunks.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_verify_bs(const DevKeyTable *__restrict__ tab,
+                                                     const uint32_t *__restrict__ ttab_img,
+                                                     const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
+                                                     uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
+                                                     uint64_t *__restrict__ stamps)
+{
+    static_assert(BLOCK / 64 <= (int)kBsMaxWaves, "LDS staging regions");
+    const uint32_t lane = threadIdx.x & 63, wv = wave_uniform(threadIdx.x / 64);
+    const uint64_t nchunks = (n + kBsChunk - 1) / kBsChunk, words32 = 2 * ((n + 63) / 64);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
+    UniformKey ukey(tab);
+    uint32_t *bits32 = reinterpret_cast<uint32_t *>(bits);
+    if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
+        for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < words32; w += (uint64_t)gridDim.x * BLOCK)
+            bits32[w] = 0;
+        return;
+    }
+    uint32_t *lds = s_bs + wv * kBsWaveDwords;
+    for (uint64_t ch = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; ch < nchunks; ch += nwaves)
+        bs_chunk(recs, stride, ch * kBsChunk, n, inf_off, hf_off, lds, tab, bits32, words32, lane);
+}
+
+// Hybrid verify (KEYSEL_ZERO): per block, NBS waves run the bitsliced VALU path on 512-record
+// chunks while the other waves run the LDS T-table path on 64-record tiles, both pulling
+// from the block's tile queue over its contiguous tile range.  Only the T-table waves wait
+// for the table fill (an LDS counter, not a block barrier), so the bitsliced waves start at
+// once.  A bitsliced wave stops claiming when fewer than kBsStop tiles would remain for the
+// T-table waves, so the block does not end on a long bitsliced chunk.
+template <int BLOCK, int NBS>
+__global__ __launch_bounds__(BLOCK) void k_verify_hybrid(const DevKeyTable *__restrict__ tab,
+                                                         const uint32_t *__restrict__ ttab_img,
+                                                         const uint8_t *__restrict__ recs, uint64_t stride,
+                                                         uint64_t n, uint32_t inf_off, uint32_t hf_off,
+                                                         uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps)
+{
+    static_assert(NBS >= 1 && NBS <= (int)kBsMaxWaves && NBS < BLOCK / 64, "wave roles");
+    constexpr uint32_t kWaves = BLOCK / 64, kTT = kWaves - NBS;
+    constexpr uint32_t kChunkTiles = kBsChunk / 64;
+    constexpr uint32_t kBsStop = kChunkTiles + 2 * kTT;
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint32_t lane = threadIdx.x & 63, wv = wave_uniform(threadIdx.x / 64);
+    const uint64_t b0 = ntiles * blockIdx.x / gridDim.x, b1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    const uint32_t count = (uint32_t)(b1 - b0);
+    const uint64_t last = n - 1;
+    UniformKey ukey(tab);
+    RecWords cur = load_rec(recs, stride, (b0 + (wv < kTT ? wv : 0)) * 64 + lane, last, inf_off, hf_off);
+    if (threadIdx.x == 0) {
+        s_next_tile = kTT;   // tiles 0..kTT-1 are the T-table waves' first tiles
+        s_fill_done = 0;
+    }
+    __syncthreads();
+    if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
+        for (uint32_t t = wv; t < count; t += kWaves)
+            if (lane == 0) bits[b0 + t] = 0;
+        return;
+    }
+    if (wv >= kTT) {   // bitsliced waves
+        uint32_t *lds = s_bs + (wv - kTT) * kBsWaveDwords;
+        uint32_t *bits32 = reinterpret_cast<uint32_t *>(bits);
+        for (;;) {
+            uint32_t t0 = count;
+            if (lane == 0) {
+                uint32_t head = __hip_atomic_load(&s_next_tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (head + kBsStop <= count) t0 = atomicAdd(&s_next_tile, kChunkTiles);
+            }
+            t0 = wave_uniform(t0);
+            if (t0 >= count) break;
+            const uint32_t t1 = t0 + kChunkTiles < count ? t0 + kChunkTiles : count;
+            const uint64_t lim = (b0 + t1) * 64 < n ? (b0 + t1) * 64 : n;
+            bs_chunk(recs, stride, (b0 + t0) * 64, lim, inf_off, hf_off, lds, tab, bits32, 2 * (b0 + t1), lane);
+        }
+        return;
+    }
+    // T-table waves: share the table fill, then wait on the LDS counter (acquire) for all of it
+    {
+        const int nw = kTT;
+        char *ldst = reinterpret_cast<char *>(s_tab64);
+        for (int ch = wv; ch < 64; ch += nw) {
+            const char *src = reinterpret_cast<const char *>(ttab_img) + ch * 1024 + lane * 16;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(ldst + ch * 1024), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(&s_fill_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&s_fill_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kTT)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_s_setprio(3);   // issue ahead of the bitsliced waves on a shared SIMD
+    const Lane l = lane_bases();
+    uint32_t t = wv;
+    while (t < count) {
+        uint32_t nt = 0;
+        if (lane == 0) nt = atomicAdd(&s_next_tile, 1u);
+        nt = wave_uniform(nt);
+        RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
+        RecWords c1[1] = {cur};
+        verify_tiles<HFV_KEYSEL_ZERO, 2, 1>(c1, b0 + t, 0, n, lane, l, &ukey, bits);
+        cur = nxt;
+        t = nt;
     }
 }
 
@@ -490,6 +727,19 @@ using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8
 template <int KEYSEL>
 static VerifyKernel pick_verify(const KernelVariant &v)
 {
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {   // bitsliced paths: one key for all lanes
+        if (v.bs == kBsOnly) return v.block == 256 ? k_verify_bs<256> : nullptr;
+        if (v.bs > 0) {
+            if (v.block != 1024 || !v.dma || v.tab != 2 || v.np != 1) return nullptr;
+            if (v.bs == 1) return k_verify_hybrid<1024, 1>;
+            if (v.bs == 2) return k_verify_hybrid<1024, 2>;
+            if (v.bs == 3) return k_verify_hybrid<1024, 3>;
+            if (v.bs == 4) return k_verify_hybrid<1024, 4>;
+            return nullptr;
+        }
+    } else {
+        if (v.bs) return nullptr;
+    }
 #define HFV_V(B, P, T)                                                                          \
     if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1 && v.dyn)                        \
         return k_verify_records<KEYSEL, B, P, T, 1, 1, 0, 1>;                                           \
@@ -587,6 +837,7 @@ static void parse_variant(const char *env, KernelVariant *v)
         else if (sscanf(p, "dma=%d", &val) == 1) v->dma = val;
         else if (sscanf(p, "np=%d", &val) == 1) v->np = val;
         else if (sscanf(p, "dyn=%d", &val) == 1) v->dyn = val;
+        else if (sscanf(p, "bs=%d", &val) == 1) v->bs = val;
         const char *c = strchr(p, ',');
         if (!c) break;
         p = c + 1;
@@ -598,6 +849,8 @@ static int finish_variant(int keysel, KernelVariant *v)
     VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(*v) : pick_verify<HFV_KEYSEL_ZERO>(*v);
     if (!k) return (int)hipErrorInvalidConfiguration;
     int lds = (v->tab == 4 ? 131072 : 65536) + (keysel == HFV_KEYSEL_IFID ? (int)sizeof(uint4) * kDevKeyRows * HFV_MAX_KEYS + 32 : 0);
+    if (v->bs == kBsOnly) lds = (int)sizeof(s_bs);
+    else if (v->bs > 0) lds += (int)sizeof(s_bs);
     int by_lds = (160 * 1024) / lds;
     int by_waves = 32 / (v->block / 64);
     int occ = 0;
@@ -622,8 +875,8 @@ int query_geometry(int device, LaunchGeom *g)
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 1};
-    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 1};
+    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 1, 0};
+    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 1, 0};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
     int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);

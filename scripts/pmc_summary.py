@@ -20,7 +20,7 @@ def main(d, sizes, kernel="k_verify_records"):
             e["name"] = r["Kernel_Name"]
             e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
         group, first = -1, False
-        if kernel != "k_verify_records":   # one batch size: every launch of `kernel` but the first
+        if not kernel.startswith("k_verify"):   # one batch size: every launch of `kernel` but the first
             group, first = 0, True
         for did in sorted(disp):
             e = disp[did]

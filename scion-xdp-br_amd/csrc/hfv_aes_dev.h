@@ -36,15 +36,17 @@ constexpr uint32_t SEL_B0 = sel_byte(0), SEL_B1 = sel_byte(1), SEL_B2 = sel_byte
 
 __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 
-template <int TAB>
-__device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, uint32_t sel)
-{
-    uint32_t a = __builtin_amdgcn_perm(w, base, sel);
-    if constexpr (TAB == 4)
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab128) + a);
-    else
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab64) + a);
-}
+// Round-table lookup of state byte K of w in the table whose lane-copy base is `base`.  The
+// LDS byte address is one v_perm_b32: state byte K -> address byte 1, the lane's copy/table
+// bits -> byte 0 (and byte 2 for T2/T3).  v_perm issues at half the rate of v_bitop3 on
+// gfx950 (scripts/ubench/valu_rate.hip), but the full-rate alternative (a shift + a
+// (v & 0xff00) | base bitop3 per byte: 7 issue slots per state word instead of 8) measured
+// slower in the kernel (2^24 records: 257.5 vs 235.5 us, profiles/r01/addr_bitop3.log): the
+// verify loop is bound by LDS issue and the lookup chain's latency, not by VALU throughput,
+// and the second dependent instruction lengthens the address -> ds_read chain.
+struct Lane;
+template <int TAB, int K>
+__device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l);
 
 template <int TAB>
 __device__ __forceinline__ void fill_ttab()
@@ -62,6 +64,22 @@ __device__ __forceinline__ void fill_ttab()
 // Same table image copied from a prebuilt global copy (ctx->ttab_img, L2-resident after the
 // first blocks) by LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB per wave-instruction
 // straight into LDS, no VGPR round trip and ~16x fewer instructions than fill_ttab.
+// Issue-only form with the block size known at compile time (reading blockDim would add a
+// dispatch-packet load whose wait also drains the record loads issued before the fill).
+template <int TAB, int BLOCK>
+__device__ __forceinline__ void fill_ttab_dma_issue(const uint32_t *__restrict__ img)
+{
+    constexpr int kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    constexpr int nw = BLOCK / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
+    for (int c = wave; c < kChunks; c += nw) {
+        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
+    }
+}
+
 template <int TAB>
 __device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
 {
@@ -95,6 +113,15 @@ struct Lane {
     uint32_t f01, f23;         // final-round byte-gather selectors
 };
 
+template <int TAB, int K>
+__device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l)
+{
+    static_assert(K >= 0 && K < 4, "state byte");
+    const uint32_t a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
+    const char *t = TAB == 4 ? reinterpret_cast<const char *>(s_tab128) : reinterpret_cast<const char *>(s_tab64);
+    return *reinterpret_cast<const uint32_t *>(t + a);
+}
+
 // Materialise a constant in a VGPR.  v_perm_b32 (VOP3 on gfx9) takes no literal, so its
 // selectors would otherwise occupy SGPRs; the SGPR-resident round keys already bring the
 // kernel close to the 80-SGPR line above which a SIMD holds fewer than 8 waves.
@@ -120,15 +147,15 @@ __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const
     uint32_t n[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b1, l.s1);
+        uint32_t a = tlu<TAB, 0>(s[c], l.b0, l);
+        uint32_t b = tlu<TAB, 1>(s[(c + 1) & 3], l.b1, l);
         if constexpr (TAB == 4) {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b2, l.s2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b3, l.s3);
+            uint32_t x = tlu<TAB, 2>(s[(c + 2) & 3], l.b2, l);
+            uint32_t d = tlu<TAB, 3>(s[(c + 3) & 3], l.b3, l);
             n[c] = xor3(xor3(a, b, x), d, r[c]);
         } else {
-            uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
-            uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b1, l.s3);
+            uint32_t x = tlu<TAB, 2>(s[(c + 2) & 3], l.b0, l);
+            uint32_t d = tlu<TAB, 3>(s[(c + 3) & 3], l.b1, l);
             n[c] = xor3(a, b, rot16(xor3(x, d, r[c])));
         }
     }
@@ -143,15 +170,15 @@ __device__ __forceinline__ void round1_macinput(uint32_t s[4], const uint4 &rk1p
 {
     uint32_t n0, n1, n2, n3;
     if constexpr (TAB == 4) {
-        n0 = xor3(tlu<TAB>(s[1], l.b1, l.s1), tlu<TAB>(s[2], l.b2, l.s2), rk1p.x);
-        n1 = xor3(xor3(tlu<TAB>(s[1], l.b0, l.s0), tlu<TAB>(s[2], l.b1, l.s1), tlu<TAB>(s[0], l.b3, l.s3)), rk1p.y, 0u);
-        n2 = xor3(xor3(tlu<TAB>(s[3], l.b1, l.s1), tlu<TAB>(s[0], l.b2, l.s2), tlu<TAB>(s[1], l.b3, l.s3)), rk1p.z, 0u);
-        n3 = xor3(xor3(tlu<TAB>(s[3], l.b0, l.s0), tlu<TAB>(s[1], l.b2, l.s2), tlu<TAB>(s[2], l.b3, l.s3)), rk1p.w, 0u);
+        n0 = xor3(tlu<TAB, 1>(s[1], l.b1, l), tlu<TAB, 2>(s[2], l.b2, l), rk1p.x);
+        n1 = xor3(xor3(tlu<TAB, 0>(s[1], l.b0, l), tlu<TAB, 1>(s[2], l.b1, l), tlu<TAB, 3>(s[0], l.b3, l)), rk1p.y, 0u);
+        n2 = xor3(xor3(tlu<TAB, 1>(s[3], l.b1, l), tlu<TAB, 2>(s[0], l.b2, l), tlu<TAB, 3>(s[1], l.b3, l)), rk1p.z, 0u);
+        n3 = xor3(xor3(tlu<TAB, 0>(s[3], l.b0, l), tlu<TAB, 2>(s[1], l.b2, l), tlu<TAB, 3>(s[2], l.b3, l)), rk1p.w, 0u);
     } else {
-        n0 = xor3(tlu<TAB>(s[1], l.b1, l.s1), rot16(tlu<TAB>(s[2], l.b0, l.s2)), rk1p.x);
-        n1 = xor3(tlu<TAB>(s[1], l.b0, l.s0), tlu<TAB>(s[2], l.b1, l.s1), rk1p.y) ^ rot16(tlu<TAB>(s[0], l.b1, l.s3));
-        n2 = xor3(tlu<TAB>(s[3], l.b1, l.s1), rot16(tlu<TAB>(s[0], l.b0, l.s2) ^ tlu<TAB>(s[1], l.b1, l.s3)), rk1p.z);
-        n3 = xor3(tlu<TAB>(s[3], l.b0, l.s0), rot16(tlu<TAB>(s[1], l.b0, l.s2) ^ tlu<TAB>(s[2], l.b1, l.s3)), rk1p.w);
+        n0 = xor3(tlu<TAB, 1>(s[1], l.b1, l), rot16(tlu<TAB, 2>(s[2], l.b0, l)), rk1p.x);
+        n1 = xor3(tlu<TAB, 0>(s[1], l.b0, l), tlu<TAB, 1>(s[2], l.b1, l), rk1p.y) ^ rot16(tlu<TAB, 3>(s[0], l.b1, l));
+        n2 = xor3(tlu<TAB, 1>(s[3], l.b1, l), rot16(tlu<TAB, 2>(s[0], l.b0, l) ^ tlu<TAB, 3>(s[1], l.b1, l)), rk1p.z);
+        n3 = xor3(tlu<TAB, 0>(s[3], l.b0, l), rot16(tlu<TAB, 2>(s[1], l.b0, l) ^ tlu<TAB, 3>(s[2], l.b1, l)), rk1p.w);
     }
     s[0] = n0; s[1] = n1; s[2] = n2; s[3] = n3;
 }
@@ -163,10 +190,10 @@ __device__ __forceinline__ void round_last_full(uint32_t s[4], const uint4 &rk, 
     const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t a = tlu<TAB>(s[c], l.b0, l.s0);
-        uint32_t b = tlu<TAB>(s[(c + 1) & 3], l.b0, l.s1);
-        uint32_t x = tlu<TAB>(s[(c + 2) & 3], l.b0, l.s2);
-        uint32_t d = tlu<TAB>(s[(c + 3) & 3], l.b0, l.s3);
+        uint32_t a = tlu<TAB, 0>(s[c], l.b0, l);
+        uint32_t b = tlu<TAB, 1>(s[(c + 1) & 3], l.b0, l);
+        uint32_t x = tlu<TAB, 2>(s[(c + 2) & 3], l.b0, l);
+        uint32_t d = tlu<TAB, 3>(s[(c + 3) & 3], l.b0, l);
         out[c] = xor3(__builtin_amdgcn_perm(b, a, l.f01), __builtin_amdgcn_perm(d, x, l.f23), r[c]);
     }
 }
@@ -177,10 +204,10 @@ template <int TAB>
 __device__ __forceinline__ void round_last_48(const uint32_t s[4], const uint4 &rk, const Lane &l, uint32_t &t0,
                                               uint32_t &t1)
 {
-    uint32_t a = tlu<TAB>(s[0], l.b0, l.s0), b = tlu<TAB>(s[1], l.b0, l.s1);
-    uint32_t x = tlu<TAB>(s[2], l.b0, l.s2), d = tlu<TAB>(s[3], l.b0, l.s3);
+    uint32_t a = tlu<TAB, 0>(s[0], l.b0, l), b = tlu<TAB, 1>(s[1], l.b0, l);
+    uint32_t x = tlu<TAB, 2>(s[2], l.b0, l), d = tlu<TAB, 3>(s[3], l.b0, l);
     t0 = xor3(__builtin_amdgcn_perm(b, a, l.f01), __builtin_amdgcn_perm(d, x, l.f23), rk.x);
-    uint32_t a1 = tlu<TAB>(s[1], l.b0, l.s0), b1 = tlu<TAB>(s[2], l.b0, l.s1);
+    uint32_t a1 = tlu<TAB, 0>(s[1], l.b0, l), b1 = tlu<TAB, 1>(s[2], l.b0, l);
     t1 = __builtin_amdgcn_perm(b1, a1, l.f01) ^ rk.y;
 }
 

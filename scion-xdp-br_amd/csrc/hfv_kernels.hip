@@ -141,8 +141,10 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
 }
 
 // STAMP = 1 is a diagnostic build: lane 0 of every wave records s_memrealtime (100 MHz,
-// chip-wide) at entry, after the table fill, after each of its first 12 tiles and at exit
-// into stamps[wave * 16 + k].  Nothing else reads the stamps.
+// chip-wide) at entry, after the table fill, after each of its first 10 tiles (12 in the
+// static variant) and at exit into stamps[wave * 16 + k]; the dynamic variant also records
+// s_memtime after the fill and at exit (slots 12, 13) for the in-kernel clock.  Nothing
+// else reads the stamps.
 // Dynamic variant: block b owns the contiguous tile range [b*T/G, (b+1)*T/G) and its waves
 // pull tiles from an LDS counter, so waves that the LDS arbiter serves less often simply
 // take fewer tiles instead of finishing last (static assignment left the last ~20 % of the
@@ -163,17 +165,29 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
     const uint32_t kWaves = BLOCK / 64;
     // first tile of each wave is static (wave index); the queue hands out the rest
     uint32_t t = wave_uniform(threadIdx.x / 64);
-    RecWords cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
     UniformKey ukey(tab);
     if (threadIdx.x == 0) s_next_tile = kWaves;
-    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
-    else fill_ttab<TAB>();
+    // The wave's first records and its share of the table pieces are in flight together;
+    // one vmcnt(0) then covers both (the table must be complete before the barrier).
+    // (Waiting at the barrier only for the table, and for the records after it, needs the
+    // record loads pinned ahead of the barrier and the waitcnt pass told that the LDS-DMA
+    // writes are done; every form tried made the compiler drain the prefetch each tile.)
+    RecWords cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+    if constexpr (DMA) {
+        fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        fill_ttab<TAB>();
+    }
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
     int nst = 0;
     if constexpr (STAMP) {
-        if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            st[1] = __builtin_amdgcn_s_memrealtime();
+            st[12] = __builtin_amdgcn_s_memtime();   // shader clock, for the in-kernel frequency
+        }
     }
     const UniformKey *ukp = nullptr;
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
@@ -192,7 +206,7 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
         RecWords c1[1] = {cur};
         verify_tiles<KEYSEL, TAB, 1>(c1, b0 + t, 0, n, lane, l, ukp, bits);
         if constexpr (STAMP) {
-            if (lane == 0 && nst < 12) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0 && nst < 10) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
             ++nst;
         }
         cur = nxt;
@@ -200,6 +214,7 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
     }
     if constexpr (STAMP) {
         if (lane == 0) {
+            st[13] = __builtin_amdgcn_s_memtime();
             st[15] = __builtin_amdgcn_s_memrealtime();
             st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                      ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
@@ -483,8 +498,12 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     }
     UniformKey ukey(tab);
 
-    if constexpr (DMA) fill_ttab_dma<TAB>(ttab_img);
-    else fill_ttab<TAB>();
+    if constexpr (DMA) {
+        fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        fill_ttab<TAB>();
+    }
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
     const Lane l = lane_bases();
@@ -875,7 +894,7 @@ int query_geometry(int device, LaunchGeom *g)
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{1024, 1, 2, 1, 1, 1, 1, 0};
+    g->single = KernelVariant{1024, 1, 4, 1, 1, 1, 1, 0};
     g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 1, 0};
     parse_variant(getenv("HFV_KVARIANT"), &g->single);
     parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);

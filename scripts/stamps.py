@@ -47,9 +47,7 @@ def main():
             fill = (s[:, 1] - s[:, 0]) * TICK_US
             end = (s[:, 15] - t0) * TICK_US
             tiles = []
-            for k in range(12):
-                if 2 + k == 14:
-                    break
+            for k in range(10):
                 m = s[:, 2 + k] != 0
                 if not m.any():
                     break
@@ -60,6 +58,7 @@ def main():
                         "fill_us_p50_max": [round(float(np.median(fill)), 2), round(float(fill.max()), 2)],
                         "tile_us_median_each": [round(x, 2) for x in tiles],
                         "last_wave_end_us": round(float(end.max()), 2),
+                        "clock_mhz_p50": round(float(np.median((s[:, 13] - s[:, 12]) / np.maximum(1, s[:, 15] - s[:, 1]) * 100.0)), 1),
                         "wave_life_us_p50": round(float(np.median((s[:, 15] - s[:, 0]) * TICK_US)), 2)})
         print(f"n={n}", json.dumps(res[-1]))
         # placement analysis of the last repetition

@@ -135,9 +135,11 @@ int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_in
  * Used by the benchmark to price the kernel against its roofline. */
 int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                              void *stream, float *kernel_ms);
-/* Host-memory batch (config 5 path): records and bitmap in HOST memory; the call stages
- * them through pinned buffers with H2D / kernel / D2H overlapped over chunks and returns
- * when pass_bits is complete. */
+/* Host-memory batch (config 5 path): records and bitmap in HOST memory; returns when
+ * pass_bits is complete.  Pageable records are staged through pinned buffers with H2D /
+ * kernel / D2H overlapped over chunks; records inside a buffer registered with
+ * hfv_host_register (an RX ring) are read by the kernel in place over PCIe (zero-copy),
+ * and a registered pass_bits is written in place. */
 int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits);
 
 /* ---- key-schedule kernels ------------------------------------------------------------

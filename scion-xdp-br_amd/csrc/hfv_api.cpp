@@ -911,8 +911,40 @@ int hfv_host_unregister(hfv_ctx *ctx, void *ptr)
     return fail(-EINVAL, "buffer was not registered with this ctx");
 }
 
+// Zero-copy host batch: the records lie in a registered (mapped) host buffer, so one verify
+// launch reads each record's INF/HF words across PCIe itself (20 of the 64 bytes; no bulk
+// H2D copy).  The bitmap is written in place when it is registered too, else to a device
+// buffer and copied back.
+static int verify_records_zero_copy(hfv_ctx *ctx, const uint8_t *drecs, size_t stride, size_t n, uint64_t *pass_bits)
+{
+    hipStream_t st = ctx->stream;
+    const size_t words = (n + 63) / 64;
+    uint64_t *dbits = (uint64_t *)host_dev_ptr(ctx, pass_bits, words * 8);
+    if (!dbits) {
+        if (ctx->zc_cap < words * 8) {
+            if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
+            ctx->zc_meta = nullptr;
+            ctx->zc_cap = 0;
+            HIP_TRY(hipMalloc((void **)&ctx->zc_meta, words * 8));
+            ctx->zc_cap = words * 8;
+        }
+        dbits = (uint64_t *)ctx->zc_meta;
+    }
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_verify_records(ctx->geom, &ds->keys, ctx->keysel, drecs, stride, n, ctx->inf_off, ctx->hf_off,
+                                  dbits, st);
+    rc = after_launch(ctx, st, e, "verify_records launch (zero-copy)");
+    if (rc) return rc;
+    if (dbits == (uint64_t *)ctx->zc_meta) HIP_TRY(hipMemcpyAsync(pass_bits, dbits, words * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
-// streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.
+// streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.  Records
+// in a registered buffer (hfv_host_register) take the zero-copy path instead.
 int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
@@ -920,7 +952,10 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
     if (!recs || !pass_bits) return fail(-EINVAL, "null buffer");
     if ((stride & 7) || stride < (size_t)ctx->hf_off + 12 || stride < (size_t)ctx->inf_off + 8)
         return fail(-EINVAL, "bad stride %zu", stride);
+    if (((uintptr_t)recs & 7) || ((uintptr_t)pass_bits & 7)) return fail(-EINVAL, "records and bitmap must be 8-byte aligned");
     DeviceGuard g(ctx->device);
+    if (const uint8_t *drecs = host_dev_ptr(ctx, recs, (n - 1) * stride + ctx->hf_off + 12))
+        return verify_records_zero_copy(ctx, drecs, stride, n, pass_bits);
     const size_t chunk = (size_t)1 << 20;   // records per chunk (64 MiB at 64 B)
     if (ctx->host_chunk < chunk * stride) {
         for (int i = 0; i < 2; ++i) {

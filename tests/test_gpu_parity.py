@@ -241,6 +241,42 @@ def test_host_path_matches_device(ctx):
     assert np.array_equal(hbits, bits_np(dbits, n))
 
 
+def test_host_zero_copy_ring(ctx):
+    """Records in a registered host ring are verified in place (zero-copy), with the bitmap
+    either registered (written in place) or pageable (copied back); both equal the device
+    path, also for a ragged count and a record range that starts inside the ring."""
+    ctx.key_add(0, orc.KEY_1111)
+    n = 100_003
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=DEV)
+    ctx.gen_records(recs, n, orc.SEED_RECORDS)
+    dbits = new_bits(n)
+    ctx.verify_records(recs, n, dbits)
+    want = bits_np(dbits, n)
+    ring = hfv.host_array((n, 64), np.uint8)
+    ring[:] = recs.cpu().numpy()
+    rbits = hfv.host_array(((n + 63) // 64,), np.uint64)
+    ctx.host_register(ring)
+    ctx.host_register(rbits)
+    try:
+        ctx.verify_records_host(ring, n, rbits)
+        assert np.array_equal(rbits, want)
+        pbits = np.zeros_like(want)
+        ctx.verify_records_host(ring, n, pbits)
+        assert np.array_equal(pbits, want)
+        sub = ring[333:]                         # a window starting inside the ring
+        m = len(sub)
+        sbits = np.zeros((m + 63) // 64, dtype=np.uint64)
+        ctx.verify_records_host(sub, m, sbits)
+        dsub = new_bits(m)
+        ctx.verify_records(recs[333:], m, dsub)
+        assert np.array_equal(sbits, bits_np(dsub, m))
+        hk, valid = orc.key_table(orc.KEY_1111)
+        assert np.array_equal(sbits[:64], orc.verify_records(np.array(sub[:4096]), hk, valid, 0))
+    finally:
+        ctx.host_unregister(ring)
+        ctx.host_unregister(rbits)
+
+
 def test_empty_and_bad_arguments(ctx):
     ctx.key_add(0, orc.KEY_1111)
     bits = new_bits(1)

@@ -5,14 +5,19 @@ records (BASELINE.json metric; config 2 = 2^20 records, single AS key, per GPU).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--keysel zero|ifid] [--n N]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-One process per GPU.  A "step" is one hfv_verify_records launch over the rank's resident
-batch of n records (weak scaling: every rank verifies its own n records, no collective on
-the data path; RCCL is used only for the timing barrier and max-over-ranks).  Rank 0
-prints one JSON line.  Besides the contract fields it carries:
-  roofline      -- the verify kernel's algorithmic bytes (64 B read + 1/8 B verdict per
-                   record) per launch / its mean launch duration (HIP events on the launch
-                   stream), against the 8 TB/s HBM3E peak; `traffic` is the PMC-measured HBM
-                   bytes per launch from profiles/ when a matching pass exists.
+One process per GPU.  A "step" is one pass of the verifier over the rank's resident batch
+of n records (weak scaling: every rank verifies its own n records, no collective on the
+data path; RCCL is used only for the timing barrier and max-over-ranks).  By default
+(--mode launch) a step is one hfv_verify_records launch; --mode service posts the K
+batches one by one to the resident service (hfv_service_submit) with starting and
+stopping its grid inside the timed region (both are always measured and reported:
+`per_launch`, `service`).  Rank 0 prints one JSON line.  Besides
+the contract fields it carries:
+  roofline      -- the headline kernel's algorithmic bytes (64 B read + 1/8 B verdict per
+                   record) / its duration from the dispatch's own start/stop events (the
+                   service grid's lifetime over all K batches, or the mean launch), against
+                   the 8 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per batch
+                   from profiles/ when a matching pass exists.
   cpu_baseline  -- the reference's own aes.c soft path (oracle/_ref, built from
                    /root/reference) over a sample of the same records on this host's cores,
                    verdicts cross-checked against the GPU bitmap.
@@ -100,6 +105,25 @@ def kernel_ms(ctx, recs, n, bits, stream, reps):
     start/stop timestamps (hipExtLaunchKernel events, hfv_verify_records_timed)."""
     ts = sorted(ctx.verify_records_timed(recs, n, bits, stream=stream) for _ in range(reps))
     return float(np.mean(ts)), float(ts[len(ts) // 2])
+
+
+def timed_steps(world, steps, fn):
+    """Run fn `steps` times between barrier + device sync on both sides; max over ranks."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def pmc_traffic(keysel, n):
@@ -386,6 +410,8 @@ def main():
     ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
                     help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
                          "br-host: config 5")
+    ap.add_argument("--mode", choices=["service", "launch"], default="launch",
+                    help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")
     ap.add_argument("--no-register", action="store_true", help="br-host: leave the ring unregistered (DMA windows)")
     args = ap.parse_args()
@@ -413,30 +439,56 @@ def main():
     ctx.gen_records(recs, n, SEED_RECORDS, first_index=rank * n, stream=stream)
     bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
 
+    # --- launch path (hfv_verify_records: one launch + table fill per batch) ---------------
     for _ in range(args.warmup):
         ctx.verify_records(recs, n, bits, stream=stream)
     torch.cuda.synchronize()
     # the verdicts must be right before anything is timed
     assert popcount(bits) == expected_pass_count(n, rank * n), "verify bitmap disagrees with generator truth"
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.verify_records(recs, n, bits, stream=stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    launch_elapsed = timed_steps(world, args.steps, lambda: ctx.verify_records(recs, n, bits, stream=stream))
     k_mean, k_med = kernel_ms(ctx, recs, n, bits, stream, max(20, min(args.steps, 200)))
+
+    # --- resident service (hfv_service_*: persistent grid, host descriptor ring) ----------
+    # The timed region starts the grid, posts the K batches one by one and stops it, so the
+    # launch, the table fill and the drain are all inside it.
+    bits.zero_()
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        ctx.service_submit(recs, n, bits)
+    ctx.service_stop()
+    assert popcount(bits) == expected_pass_count(n, rank * n), "service bitmap disagrees with generator truth"
+    svc = {}
+
+    def service_run():
+        ctx.service_start()
+        for _ in range(args.steps):
+            ctx.service_submit(recs, n, bits)
+        svc["grid_ms"] = ctx.service_stop()
+
+    svc_elapsed = timed_steps(world, 1, service_run)
+    assert popcount(bits) == expected_pass_count(n, rank * n)
+    headline = args.mode
+    elapsed = svc_elapsed if headline == "service" else launch_elapsed
+
     bytes_per_launch = hfv.BYTES_PER_PACKET * n
-    achieved = bytes_per_launch / (k_mean * 1e-3) / 1e9
+    if headline == "service":
+        # the grid's lifetime (dispatch start/stop events) covers all K batches
+        grid_s = svc["grid_ms"] * 1e-3
+        achieved = bytes_per_launch * args.steps / grid_s / 1e9
+        kern = {"kernel": "k_verify_service", "grid_ms": round(svc["grid_ms"], 4),
+                "batches_per_grid": args.steps, "kernel_ms_per_batch": round(svc["grid_ms"] / args.steps, 5),
+                "algorithmic_bytes_per_grid": int(bytes_per_launch * args.steps)}
+    else:
+        achieved = bytes_per_launch / (k_mean * 1e-3) / 1e9
+        kern = {"kernel": "k_verify_records", "kernel_ms_mean": round(k_mean, 5),
+                "kernel_ms_median": round(k_med, 5), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    per_launch = {"mpkts": round(world * n * args.steps / launch_elapsed / 1e6, 2),
+                  "ms_per_step": round(launch_elapsed / args.steps * 1e3, 5),
+                  "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(k_med, 5),
+                  "kernel_mpkts": round(n / k_mean / 1e3, 1),
+                  "frac": round(bytes_per_launch / (k_mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    service = {"mpkts": round(world * n * args.steps / svc_elapsed / 1e6, 2),
+               "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4)}
 
     traffic = pmc_traffic(args.keysel, n)
 
@@ -457,12 +509,15 @@ def main():
                                f"{'256 ingress-interface keys (KEYSEL_IFID)' if keysel else 'single AS key'}",
                    "records_per_gpu": n, "record_bytes": 64, "keysel": args.keysel,
                    "parallelism": f"batch-sharded x{world}, no collective"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_verify_records", "variant": ctx.describe(), "kernel_ms_mean": round(k_mean, 5),
-                     "kernel_ms_median": round(k_med, 5),
-                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                     "note": f"2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"},
+        "roofline": dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}, **kern,
+                         variant=ctx.describe(),
+                         note="2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"),
+        "path": ("resident service: one persistent grid, the K batches posted one by one through the host "
+                 "descriptor ring (hfv_service_submit); grid launch, table fill and drain inside the timed region"
+                 if headline == "service" else "one hfv_verify_records launch per batch"),
+        "service": service,
+        "per_launch": per_launch,
     }
 
     if rank == 0 and world == 1 and args.big_n:
@@ -476,9 +531,20 @@ def main():
         assert popcount(bbits) == expected_pass_count(nb, 0)
         bm, bmed = kernel_ms(ctx, big, nb, bbits, stream, 20)
         ach = hfv.BYTES_PER_PACKET * nb / (bm * 1e-3) / 1e9
+        # the same batch through the resident service, 10 batches per grid
+        bbits.zero_()
+        ctx.service_start()
+        for _ in range(10):
+            ctx.service_submit(big, nb, bbits)
+        sg = ctx.service_stop()
+        assert popcount(bbits) == expected_pass_count(nb, 0)
+        sach = hfv.BYTES_PER_PACKET * nb * 10 / (sg * 1e-3) / 1e9
         result["hbm_resident"] = {"records": nb, "kernel_ms_mean": round(bm, 4), "mpkts": round(nb / bm / 1e3, 1),
                                   "achieved_GBs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                                  "traffic": pmc_traffic(args.keysel, nb)}
+                                  "traffic": pmc_traffic(args.keysel, nb),
+                                  "service_ms_per_batch": round(sg / 10, 4),
+                                  "service_mpkts": round(nb * 10 / sg / 1e3, 1),
+                                  "service_frac": round(sach / HBM_PEAK_GBS, 4)}
         del big, bbits
 
     if rank == 0 and world == 1 and not args.no_host_e2e:

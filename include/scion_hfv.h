@@ -142,6 +142,41 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
  * and a registered pass_bits is written in place. */
 int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits);
 
+/* ---- resident verify service -----------------------------------------------------------
+ * The GPU counterpart of the XDP program staying attached to the interface
+ * (border_router, xdp.c:250-284, runs for every packet without a per-packet load): one
+ * persistent grid per ctx keeps the AES tables (and, for KEYSEL_IFID, the key image)
+ * resident in LDS and verifies batches as the host posts them, with the same verdict
+ * semantics as hfv_verify_records.  Batches are posted into a 64-entry descriptor ring in
+ * pinned host memory; no kernel launch or table fill per batch, and a batch's tail
+ * overlaps the next batch's start.
+ *   - Key-table, keysel or record-layout changes take effect at the next submit (the
+ *     service is restarted there, after the batches already posted: a batch boundary).
+ *   - Any other data-path call on the ctx (hfv_verify_records, hfv_br_process, ...) first
+ *     stops the service after its posted batches; the next submit starts it again.
+ *   - The grid exits by itself after idle_ms without a new batch (default 1000 ms), so a
+ *     host that disappears never leaves it running; a later submit restarts it.
+ *   - While the service runs it holds every CU's LDS: other kernels on this GPU wait for it
+ *     to stop. */
+/* Launch the service grid (no-op if running).  idle_ms 0: 1000 ms. */
+int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms);
+/* Post one batch (device pointers, as hfv_verify_records; starts the service if needed).
+ * Returns its ticket (1, 2, ...) in *ticket.  Blocks only while 64 batches are in flight.
+ * Host-ordered, not stream-ordered: the records must be in place and the bitmap must no
+ * longer be written by other work when the call is made (synchronize their producers). */
+int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                       uint64_t *ticket);
+/* 1 if the ticket's verdicts are complete in pass_bits (visible to any stream and to
+ * copies), 0 if not yet. */
+int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket);
+/* Wait until the ticket is complete; timeout_ms < 0 waits indefinitely.  -ETIMEDOUT on
+ * timeout, -EIO if the service stopped before completing it. */
+int hfv_service_wait(hfv_ctx *ctx, uint64_t ticket, int timeout_ms);
+/* Finish the posted batches and stop the grid; *kernel_ms (nullable) receives the grid's
+ * lifetime (dispatch start/stop events).  -ETIMEDOUT if it had exited on its idle timeout. */
+int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms);
+int hfv_service_running(const hfv_ctx *ctx);
+
 /* ---- key-schedule kernels ------------------------------------------------------------
  * AES-128 key expansion + CMAC K1 on the GPU, one key per lane: device raw keys[n] ->
  * device hop_keys[n] (same bytes as aes_key_expansion + aes_cmac_subkeys). */

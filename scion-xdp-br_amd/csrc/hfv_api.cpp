@@ -176,7 +176,27 @@ struct hfv_ctx {
     int nhreg = 0;
     uint8_t *zc_meta = nullptr;   // zero-copy path: device len/ifindex/outputs for unregistered arrays
     size_t zc_cap = 0;
+    // resident verify service (hfv_service_*)
+    bool svc_running = false;
+    int svc_keysel = HFV_KEYSEL_ZERO;
+    uint32_t svc_inf_off = 0, svc_hf_off = 0, svc_idle_ms = 0;
+    hipStream_t svc_stream = nullptr;
+    SvcShared *svc_host = nullptr;   // descriptor ring + completions, coherent pinned memory
+    SvcShared *svc_host_dev = nullptr;
+    unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
+    uint64_t svc_next = 1;           // next ticket
+    hipEvent_t svc_ev[2] = {nullptr, nullptr};
 };
+
+// Any other data-path call on the ctx first stops a running service (after the batches
+// already posted): its grid holds every CU's LDS, so other kernels could not start until
+// it exits, and a call that waits for its own kernel would wait for the idle timeout.
+static int svc_quiesce(hfv_ctx *ctx);
+#define SVC_QUIESCE(ctx)                         \
+    do {                                         \
+        int q_ = svc_quiesce(ctx);               \
+        if (q_) return q_;                       \
+    } while (0)
 
 // NULL is HIP's default stream, as for any HIP API taking a stream.
 static hipStream_t pick_stream(hfv_ctx *, void *stream) { return (hipStream_t)stream; }
@@ -300,6 +320,14 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
 {
     if (!ctx) return 0;
     DeviceGuard g(ctx->device);
+    (void)svc_quiesce(ctx);
+    if (ctx->svc_stream) {
+        (void)hipStreamSynchronize(ctx->svc_stream);
+        (void)hipStreamDestroy(ctx->svc_stream);
+    }
+    if (ctx->svc_host) (void)hipHostFree(ctx->svc_host);
+    for (int i = 0; i < 2; ++i)
+        if (ctx->svc_ev[i]) (void)hipEventDestroy(ctx->svc_ev[i]);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int i = 0; i < 2; ++i) {
         if (ctx->hstream[i]) { (void)hipStreamSynchronize(ctx->hstream[i]); (void)hipStreamDestroy(ctx->hstream[i]); }
@@ -445,6 +473,7 @@ int hfv_key_add_batch(hfv_ctx *ctx, uint32_t first, const struct aes_key *keys, 
     if ((size_t)first + n > HFV_MAX_KEYS) return fail(-EINVAL, "slots %u..%zu exceed %d", first, first + n, HFV_MAX_KEYS);
     if (n == 0) return 0;
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     uint8_t *d_raw = nullptr;
     hop_key *d_hk = nullptr;
     HIP_TRY(hipMalloc((void **)&d_raw, 16 * n));
@@ -479,6 +508,7 @@ int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
     if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
         return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
@@ -501,6 +531,7 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
     if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
         return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     for (int i = 0; i < 2; ++i)
         if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
     hipStream_t st = pick_stream(ctx, stream);
@@ -525,6 +556,7 @@ extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n
 {
     if (!ctx || !recs || !pass_bits || !stamps || !grid || n == 0) return fail(-EINVAL, "bad argument");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
@@ -558,6 +590,7 @@ int hfv_verify_macinputs(hfv_ctx *ctx, const struct macinput *mi, const uint64_t
     if (((uintptr_t)mi & 15) || ((uintptr_t)expected & 7) || ((uintptr_t)pass_bits & 7))
         return fail(-EINVAL, "macinputs must be 16-byte aligned, expected/bitmap 8-byte aligned");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
@@ -575,6 +608,7 @@ int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_in
     if (!mi || !tags) return fail(-EINVAL, "null buffer");
     if (((uintptr_t)mi & 15) || ((uintptr_t)tags & 15)) return fail(-EINVAL, "macinputs/tags must be 16-byte aligned");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
@@ -591,6 +625,7 @@ int hfv_expand_keys(hfv_ctx *ctx, const struct aes_key *keys, size_t n, struct h
     if (!keys || !out) return fail(-EINVAL, "null buffer");
     if (((uintptr_t)keys & 15) || ((uintptr_t)out & 15)) return fail(-EINVAL, "buffers must be 16-byte aligned");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     int e = launch_expand_keys((const uint8_t *)keys, n, out, nullptr, 0, pick_stream(ctx, stream));
     if (e != hipSuccess) return hip_fail((hipError_t)e, "expand_keys launch");
     return 0;
@@ -607,6 +642,7 @@ int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t 
     if (ctx->inf_off != HFV_REC_INF_OFF || ctx->hf_off != HFV_REC_HF_OFF)
         return fail(-EINVAL, "the generator writes the default 64 B layout only");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
@@ -650,6 +686,7 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
     if (rc) return rc;
     if ((uintptr_t)stats & 7) return fail(-EINVAL, "misaligned stats");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     hipStream_t st = pick_stream(ctx, stream);
     DevState *ds;
     rc = publish_keys(ctx, st, &ds);
@@ -670,6 +707,7 @@ int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_
     if (rc) return rc;
     if ((uintptr_t)stats & 7) return fail(-EINVAL, "misaligned stats");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     for (int i = 0; i < 2; ++i)
         if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
     hipStream_t st = pick_stream(ctx, stream);
@@ -814,6 +852,7 @@ int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16
     if (window == 0) window = slot < 256 ? slot : 256;
     if (window < 64 || (window & 7) || window > slot) return fail(-EINVAL, "window must be a multiple of 8 in [64, slot]");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     uint8_t *dframes = host_dev_ptr(ctx, frames, n * slot);
     if (dframes) return br_zero_copy(ctx, dframes, slot, len, ingress_ifindex, n, action, verdict, egress_ifindex, stats);
     int rc = brh_buffers(ctx, window > slot ? slot : window);
@@ -954,6 +993,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         return fail(-EINVAL, "bad stride %zu", stride);
     if (((uintptr_t)recs & 7) || ((uintptr_t)pass_bits & 7)) return fail(-EINVAL, "records and bitmap must be 8-byte aligned");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     if (const uint8_t *drecs = host_dev_ptr(ctx, recs, (n - 1) * stride + ctx->hf_off + 12))
         return verify_records_zero_copy(ctx, drecs, stride, n, pass_bits);
     const size_t chunk = (size_t)1 << 20;   // records per chunk (64 MiB at 64 B)
@@ -1003,6 +1043,189 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
     return 0;
 }
 
+// ---- resident verify service ----------------------------------------------------------
+// The host side of k_verify_service (hfv_kernels.hip): tickets 1, 2, ... go to ring slot
+// (t - 1) % kSvcRing; ticket t is posted only once ticket t - kSvcRing is done.
+
+}  // extern "C"
+
+// Ticket t is complete when every block of the grid has reported its share of it.
+static bool svc_is_done(const hfv_ctx *ctx, uint64_t t)
+{
+    const uint64_t *d = ctx->svc_host->done[(t - 1) % kSvcRing];
+    for (unsigned k = 0; k < ctx->svc_grid; ++k)
+        if (__atomic_load_n(&d[k], __ATOMIC_ACQUIRE) < t) return false;
+    return true;
+}
+
+static int svc_wait_done(hfv_ctx *ctx, uint64_t t, int timeout_ms)
+{
+    struct timespec t0, now;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint64_t spin = 0;; ++spin) {
+        if (svc_is_done(ctx, t)) return 0;
+        if ((spin & 255) != 255) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0)
+            return fail(-EIO, "verify service exited (%s); ticket %llu will not complete",
+                        ctx->svc_host->status == kSvcIdleTimeout ? "idle timeout" : "watchdog",
+                        (unsigned long long)t);
+        if (hipStreamQuery(ctx->svc_stream) == hipSuccess)
+            return fail(-EIO, "verify service grid has exited; ticket %llu will not complete", (unsigned long long)t);
+        clock_gettime(CLOCK_MONOTONIC, &now);
+        double ms = (now.tv_sec - t0.tv_sec) * 1e3 + (now.tv_nsec - t0.tv_nsec) * 1e-6;
+        if (timeout_ms >= 0 && ms > timeout_ms)
+            return fail(-ETIMEDOUT, "ticket %llu not done after %d ms", (unsigned long long)t, timeout_ms);
+    }
+}
+
+static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint64_t stride, uint64_t *ticket)
+{
+    const uint64_t t = ctx->svc_next;
+    if (t > kSvcRing) {   // the slot's previous batch must be done (and its descriptor read)
+        int rc = svc_wait_done(ctx, t - kSvcRing, 60000);
+        if (rc) return rc;
+    }
+    SvcDesc *d = &ctx->svc_host->desc[(t - 1) % kSvcRing];
+    d->recs = recs;
+    d->bits = bits;
+    d->n = n;
+    d->stride = stride;
+    __atomic_store_n(&d->seq, t, __ATOMIC_RELEASE);
+    ctx->svc_next = t + 1;
+    if (ticket) *ticket = t;
+    return 0;
+}
+
+static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
+{
+    if (kernel_ms) *kernel_ms = 0.0f;
+    if (!ctx->svc_running) return 0;
+    const uint64_t last = ctx->svc_next - 1;   // last batch posted
+    int rc = 0;
+    if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0)
+        rc = svc_post(ctx, 0, 0, kSvcStopN, 0, nullptr);
+    // the grid exits on the stop descriptor, or on its idle timeout if the post failed
+    hipError_t e = hipStreamSynchronize(ctx->svc_stream);
+    ctx->svc_running = false;
+    if (e != hipSuccess) return hip_fail(e, "verify service");
+    if (rc) return rc;
+    if (kernel_ms) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
+    // an idle exit is clean unless it left a posted batch unverified (batches may complete
+    // out of order; only the newest kSvcRing can still be open)
+    for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t)
+        if (!svc_is_done(ctx, t))
+            return fail(-ETIMEDOUT, "verify service exited on its idle timeout before ticket %llu",
+                        (unsigned long long)t);
+    return 0;
+}
+
+static int svc_quiesce(hfv_ctx *ctx) { return ctx->svc_running ? svc_stop(ctx, nullptr) : 0; }
+
+static bool svc_keys_changed(hfv_ctx *ctx)
+{
+    return ctx->dirty || (ctx->keymap && keymap_seq(ctx->keymap) != ctx->keymap_seq);
+}
+
+extern "C" {
+
+int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (ctx->svc_running) return 0;
+    DeviceGuard g(ctx->device);
+    if (!ctx->svc_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
+        HIP_TRY(hipHostMalloc((void **)&ctx->svc_host, sizeof(SvcShared),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void **)&ctx->svc_host_dev, ctx->svc_host, 0));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreate(&ctx->svc_ev[i]));
+    }
+    memset(ctx->svc_host, 0, sizeof(SvcShared));
+    DevState *ds;
+    int rc = publish_keys(ctx, ctx->svc_stream, &ds);
+    if (rc) return rc;
+    ctx->svc_keysel = ctx->keysel;
+    ctx->svc_inf_off = ctx->inf_off;
+    ctx->svc_hf_off = ctx->hf_off;
+    ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
+    ctx->svc_next = 1;
+    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->inf_off, ctx->hf_off,
+                                  (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_stream, ctx->svc_ev[0],
+                                  ctx->svc_ev[1], &ctx->svc_grid);
+    rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
+    if (rc) return rc;
+    ctx->svc_running = true;
+    return 0;
+}
+
+int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                       uint64_t *ticket)
+{
+    if (!ctx || !ticket) return fail(-EINVAL, "null argument");
+    *ticket = 0;
+    if (n && (!recs || !pass_bits)) return fail(-EINVAL, "null buffer");
+    if (n >= kSvcStopN / 2) return fail(-EINVAL, "batch too large");
+    if (((uintptr_t)recs & 7) || (stride & 7) || ((uintptr_t)pass_bits & 7))
+        return fail(-EINVAL, "records, stride and bitmap must be 8-byte aligned");
+    if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
+        return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
+    DeviceGuard g(ctx->device);
+    if (ctx->svc_running && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0) {
+        // the grid left on its idle timeout (its posted batches were all done, or waits on
+        // them have reported -EIO): start a fresh one
+        (void)hipStreamSynchronize(ctx->svc_stream);
+        ctx->svc_running = false;
+    }
+    // key, key-selection or layout changes take effect at this batch boundary; the grid's
+    // batch counter is 32-bit, so the service also restarts every 2^31 batches
+    if (ctx->svc_running && (svc_keys_changed(ctx) || ctx->svc_keysel != ctx->keysel ||
+                             ctx->svc_inf_off != ctx->inf_off || ctx->svc_hf_off != ctx->hf_off ||
+                             ctx->svc_next >= (1ull << 31))) {
+        int rc = svc_stop(ctx, nullptr);
+        if (rc) return rc;
+    }
+    if (!ctx->svc_running) {
+        int rc = hfv_service_start(ctx, ctx->svc_idle_ms);
+        if (rc) return rc;
+    }
+    return svc_post(ctx, (uint64_t)(uintptr_t)recs, (uint64_t)(uintptr_t)pass_bits, n, stride, ticket);
+}
+
+int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)
+{
+    if (!ctx || !ctx->svc_host || ticket == 0 || ticket >= ctx->svc_next) return fail(-EINVAL, "unknown ticket");
+    return svc_is_done(ctx, ticket) ? 1 : 0;
+}
+
+int hfv_service_wait(hfv_ctx *ctx, uint64_t ticket, int timeout_ms)
+{
+    if (!ctx || !ctx->svc_host || ticket == 0 || ticket >= ctx->svc_next) return fail(-EINVAL, "unknown ticket");
+    if (svc_is_done(ctx, ticket)) return 0;
+    if (!ctx->svc_running) return fail(-EIO, "verify service stopped before ticket %llu", (unsigned long long)ticket);
+    return svc_wait_done(ctx, ticket, timeout_ms);
+}
+
+int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    return svc_stop(ctx, kernel_ms);
+}
+
+int hfv_service_running(const hfv_ctx *ctx) { return ctx && ctx->svc_running ? 1 : 0; }
+
+// Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
+// 0 loaded ring slot i's descriptor.
+int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
+{
+    if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
+    for (uint32_t i = 0; i < kSvcRing; ++i) out[i] = __atomic_load_n(&ctx->svc_host->load_clock[i], __ATOMIC_ACQUIRE);
+    return 0;
+}
+
 // ---- memory helpers -------------------------------------------------------------------
 
 int hfv_dev_alloc(hfv_ctx *ctx, size_t bytes, void **ptr)
@@ -1017,6 +1240,7 @@ int hfv_dev_free(hfv_ctx *ctx, void *ptr)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     HIP_TRY(hipFree(ptr));
     return 0;
 }
@@ -1025,6 +1249,7 @@ int hfv_memcpy_h2d(hfv_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return 0;
@@ -1034,6 +1259,7 @@ int hfv_memcpy_d2h(hfv_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return 0;

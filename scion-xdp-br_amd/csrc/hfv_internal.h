@@ -74,6 +74,31 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out);
 
 enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 
+// Resident verify service (hfv_service_*): the host posts batch descriptors into a ring in
+// pinned, coherent host memory; the persistent grid polls it, verifies each batch, and every
+// block publishes the completion of its share of a batch straight into host memory (one
+// posted PCIe write; the host combines the per-block flags).  Batch b (0-based, ticket b+1)
+// uses ring slot b % kSvcRing; the host posts ticket t only once ticket t - kSvcRing is
+// complete, which is what lets each block cache kSvcRing descriptors in LDS without any
+// reuse check (hfv_kernels.hip, k_verify_service).
+constexpr uint32_t kSvcRing = 64;
+constexpr uint32_t kSvcMaxBlocks = 1024;
+constexpr uint64_t kSvcStopN = ~0ull;   // descriptor n: the service exits
+struct SvcDesc {
+    uint64_t recs, bits, n, stride;   // device pointers / counts of the batch
+    uint64_t seq;                     // ticket; stored last, with release
+    uint64_t pad[3];
+};
+struct SvcShared {
+    SvcDesc desc[kSvcRing];
+    uint64_t status;                 // nonzero: the grid stopped on its own (kSvcIdleTimeout, kSvcWatchdog)
+    uint64_t pad[7];
+    uint64_t load_clock[kSvcRing];   // diagnostics: s_memrealtime when block 0 loaded the slot
+    uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = t: block k's share of t is verified
+};
+constexpr uint64_t kSvcIdleTimeout = 2;
+constexpr uint64_t kSvcWatchdog = 3;    // a wave gave up waiting for its block's loader
+
 struct KernelVariant {
     int block;           // threads per block
     int pf;              // record tiles loaded ahead of the one computed (1 or 2)
@@ -110,6 +135,12 @@ int query_geometry(int device, LaunchGeom *g);
 int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream);
 int build_ttab_image(uint32_t *img, void *stream);
+// persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
+// block waits for the next descriptor before it exits with status kSvcIdleTimeout
+// returns the grid size in *grid
+int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, uint32_t inf_off,
+                          uint32_t hf_off, uint64_t idle_ticks, void *stream, void *ev_start, void *ev_stop,
+                          unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

@@ -44,6 +44,9 @@ __global__ void k_build_ttab_image(uint32_t *__restrict__ img)
 // ---------------------------------------------------------------------------------------
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+typedef __attribute__((address_space(1))) uint8_t GlobalU8;
+typedef __attribute__((address_space(1))) uint64_t GlobalU64;
+
 struct RecWords {
     uint2 inf;    // INF bytes 0-7: flags rsv segid[2] | ts[4]
     uint2 hfa;    // HF bytes 0-7: flags exp ing[2] | eg[2] mac0 mac1
@@ -56,12 +59,32 @@ __device__ __forceinline__ RecWords load_rec(const uint8_t *recs, uint64_t strid
                                              uint32_t inf_off, uint32_t hf_off)
 {
     RecWords r;
-    const uint8_t *p = recs + (i < last ? i : last) * stride;
-    u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p + inf_off));
-    u32x2 b = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p + hf_off));
+    // global address space even when `recs` came out of memory (the service's descriptors),
+    // so these are global_load (vmcnt only), not flat loads that also count in lgkmcnt
+    const GlobalU8 *p = (const GlobalU8 *)(recs) + (i < last ? i : last) * stride;
+    u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x2 *>(p + inf_off));
+    u32x2 b = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x2 *>(p + hf_off));
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
-    r.hfb = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p + hf_off + 8));
+    r.hfb = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(p + hf_off + 8));
+    return r;
+}
+
+// Same words read with system-scope (L1/L2-bypassing, coherent) loads: what the resident
+// service uses when it may not invalidate the caches per batch (HFV_SVC_ACQ == 2).
+__device__ __forceinline__ RecWords load_rec_sys(const uint8_t *recs, uint64_t stride, uint64_t i, uint64_t last,
+                                                 uint32_t inf_off, uint32_t hf_off)
+{
+    RecWords r;
+    const uint8_t *p = recs + (i < last ? i : last) * stride;
+    uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p + inf_off), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p + hf_off), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    r.inf = make_uint2((uint32_t)a, (uint32_t)(a >> 32));
+    r.hfa = make_uint2((uint32_t)b, (uint32_t)(b >> 32));
+    r.hfb = __hip_atomic_load(reinterpret_cast<const uint32_t *>(p + hf_off + 8), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
     return r;
 }
 
@@ -93,10 +116,12 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
 // independent AES chains per lane, interleaved by the scheduler to hide LDS latency), and
 // loads its next NP tiles while it computes the current ones (PF = prefetch depth in
 // iterations).  Tiles of one wave: t, t + nwaves, t + 2*nwaves, ...
-template <int KEYSEL, int TAB, int NP>
+// RET = 1: return the ballots in ret[] instead of storing them (the resident service
+// batches its verdict stores).
+template <int KEYSEL, int TAB, int NP, int RET = 0>
 __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t t, uint64_t nwaves, uint64_t n,
                                              uint32_t lane, const Lane &l, const UniformKey *ukey,
-                                             uint64_t *__restrict__ bits)
+                                             uint64_t *__restrict__ bits, uint64_t *ret = nullptr)
 {
     uint32_t s[NP][4];
     uint32_t slot[NP];
@@ -136,7 +161,10 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
         }
         bool pass = ok && rec_tag_matches(cur[p], t0, t1);
         uint64_t ballot = __ballot(pass);
-        if (lane == 0 && t + p * nwaves < (n + 63) / 64) bits[t + p * nwaves] = ballot;
+        if constexpr (RET)
+            ret[p] = ballot;
+        else if (lane == 0 && t + p * nwaves < (n + 63) / 64)
+            ((GlobalU64 *)(bits))[t + p * nwaves] = ballot;
     }
 }
 
@@ -548,6 +576,321 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
                      ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// resident verify service (hfv_service_*): one persistent 1024-thread block per CU verifies
+// batch after batch while the round tables (and the key image) stay in LDS
+// ---------------------------------------------------------------------------------------
+// The host posts batch descriptors into a ring in coherent host memory (SvcShared,
+// hfv_internal.h).  In every batch, block k owns the contiguous tile range
+// [T*k/G, T*(k+1)/G) (T = tiles of the batch, G = grid).  Its waves claim tiles from ONE
+// block-local counter that runs on across batches: block tile number g belongs to the batch
+// b with base_b <= g < base_b + count_b, base_{b+1} = base_b + count_b (modulo 2^32).  Waves
+// roll from one batch into the next without a block barrier, so the tail of batch b
+// overlaps the start of batch b + 1, and the table fill is paid once per service instead of
+// once per batch.
+//
+// Descriptor cache: batch b sits in s_svc[b % kSvcRing].  The host posts ticket t = b + 1
+// only after ticket t - kSvcRing completed, so when a block loads batch L every batch up to
+// L - kSvcRing is verified; an unverified claim g therefore lies in one of the newest
+// kSvcRing batches and never in the slot being overwritten.
+//
+// Completion: a wave counts its verified tile in the slot's LDS counter after its verdict
+// store has drained (vmcnt(0)); the wave that completes the block's share writes the XCD's
+// L2 back (system-scope release) and bumps the batch's grid counter; the last block resets
+// it and stores the ticket into host->done with release.
+struct SvcSlot {
+    uint32_t base, count;   // block tile numbers [base, base + count)
+    uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
+    uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the block's range
+    uint64_t pad;
+};
+static __shared__ SvcSlot s_svc[kSvcRing];
+static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
+
+struct SvcTile {   // one claimed tile, wave-uniform
+    uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + (g - base)
+    uint32_t b, base, count;
+};
+enum SvcClaim { kSvcFound = 0, kSvcStop = 1, kSvcPending = 2 };
+
+__device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
+{
+    return (uint64_t)wave_uniform((uint32_t)x) | ((uint64_t)wave_uniform((uint32_t)(x >> 32)) << 32);
+}
+
+#ifndef HFV_SVC_ACQ
+#define HFV_SVC_ACQ 1   // 0: none, 1: acquire fence per loaded batch, 2: system-scope record loads
+#endif
+
+// This block's share of batch b is verified (one lane).  The verdict words were written
+// through to memory (system-scope stores) and every wave waited for its stores'
+// acknowledgement before counting its tiles, so nothing of the batch is left in L2: the
+// block reports straight to the host, no L2 writeback (buffer_wbl2 per block per batch
+// measured ~35 us per batch) and no grid-wide atomic (256 blocks on one counter serialise
+// at the memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/).
+__device__ void svc_complete(SvcShared *host, uint32_t b)
+{
+    __hip_atomic_store(&host->done[b % kSvcRing][blockIdx.x], (uint64_t)b + 1, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Load batch b into its slot (one lane, holding s_svc_lock, s_svc_loaded == b).  blocking:
+// poll until the host posts it or idle_ticks pass (then the service stops); otherwise one
+// look.  Returns false if the descriptor is not there yet.
+__device__ bool svc_load(SvcShared *host, uint32_t b, bool blocking, uint64_t idle_ticks)
+{
+    const uint32_t slot = b % kSvcRing;
+    SvcDesc *d = &host->desc[slot];
+    bool stop = false;
+    if (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)b + 1) {
+        if (!blocking) return false;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)b + 1) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                __hip_atomic_store(&host->status, kSvcIdleTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                stop = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+#if HFV_SVC_ACQ == 1
+    // the batch's records were written before the host posted it: drop stale cache lines
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+    if (blockIdx.x == 0)
+        __hip_atomic_store(&host->load_clock[slot], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    SvcSlot &s = s_svc[slot];
+    const SvcSlot &p = s_svc[(b + kSvcRing - 1) % kSvcRing];
+    s.base = b ? p.base + p.count : 0u;
+    s.done = 0;
+    uint64_t n = 0;
+    if (!stop) {
+        // the four fields in one round trip over PCIe (the ring is uncached host memory)
+        typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+        const u64x4 f = __builtin_nontemporal_load(reinterpret_cast<const u64x4 *>(&d->recs));
+        s.recs = f.x;
+        s.bits = f.y;
+        n = f.z;
+        s.stride = f.w;
+        stop = n == kSvcStopN;
+    }
+    s.stop = stop;
+    if (stop) {
+        s.count = 0;
+    } else {
+        const uint64_t ntiles = (n + 63) / 64;
+        const uint64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+        s.n = n;
+        s.tile0 = t0;
+        s.count = (uint32_t)(t1 - t0);
+        if (s.count == 0) svc_complete(host, b);
+    }
+    __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return true;
+}
+
+// The wave has just entered batch b: if batch b + 1 is not loaded yet and nobody is loading,
+// take one look for its descriptor now, so the block's waves find it loaded when they reach
+// the end of batch b instead of waiting a PCIe round trip there.
+__device__ __forceinline__ void svc_prefetch(SvcShared *host, uint64_t idle_ticks, uint32_t lane,
+                                             uint32_t b)
+{
+    if (lane == 0 && __hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1) {
+        uint32_t expect = 0;
+        if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1)
+                (void)svc_load(host, b + 1, false, idle_ticks);
+            __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// Map block tile number g to its batch (mb: batch of the wave's previous claim, g only
+// grows).  Not blocking: kSvcPending if g lies in a batch the host has not posted yet.
+__device__ __forceinline__ SvcClaim svc_map(SvcShared *host, uint64_t idle_ticks, uint32_t lane,
+                                            uint32_t g, bool blocking, uint32_t &mb, const SvcTile &hint, SvcTile &t)
+{
+    if (g - hint.base < hint.count) {   // same batch as the wave's current tile: no LDS reads
+        t = hint;
+        t.tile = hint.tile0 + (g - hint.base);
+        return kSvcFound;
+    }
+    uint64_t t_wait = 0;
+    for (;;) {
+        const uint32_t L =
+            wave_uniform(__hip_atomic_load(&s_svc_loaded, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        uint32_t lo = L > kSvcRing ? L - kSvcRing : 0u;
+        if (mb > lo) lo = mb;
+        // newest loaded batch starting at or before g
+        for (uint32_t b = L; b-- > lo;) {
+            const SvcSlot &s = s_svc[b % kSvcRing];
+            const uint32_t base = wave_uniform(s.base);
+            if ((int32_t)(g - base) < 0) continue;
+            if (wave_uniform(s.stop)) return kSvcStop;
+            const uint32_t count = wave_uniform(s.count);
+            if (g - base >= count) break;   // g is beyond the loaded batches
+            t.recs = wave_uniform64(s.recs);
+            t.bits = wave_uniform64(s.bits);
+            t.n = wave_uniform64(s.n);
+            t.stride = wave_uniform64(s.stride);
+            t.tile0 = wave_uniform64(s.tile0);
+            t.tile = t.tile0 + (g - base);
+            t.b = b;
+            t.base = base;
+            t.count = count;
+            mb = b;
+            return kSvcFound;
+        }
+        // load batch L (one loader per block at a time)
+        uint32_t r = 0;   // 1: loaded or someone else did, 2: not posted yet
+        if (lane == 0) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                r = 1;
+                if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == L &&
+                    !svc_load(host, L, blocking, idle_ticks))
+                    r = 2;
+                __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        r = wave_uniform(r);
+        if (r == 2 || (r == 0 && !blocking)) return kSvcPending;
+        if (r == 0) {
+            // watchdog: the loader is bounded by idle_ticks; never wait much longer here
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (!t_wait) t_wait = now;
+            if (now - t_wait > 2 * idle_ticks + 100000000ull) {
+                if (lane == 0)
+                    __hip_atomic_store(&host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return kSvcStop;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+
+// Count k verified tiles of batch b (count: the block's tiles in it) once their verdict
+// stores are acknowledged.  A wave defers this until its next claim leaves the batch (or
+// must wait for a descriptor), so the store-acknowledge wait is paid once per batch per
+// wave instead of once per tile.
+__device__ __forceinline__ void svc_count(SvcShared *host, uint32_t lane, uint32_t b, uint32_t count,
+                                          uint32_t k)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the verdict words are acknowledged
+    if (lane == 0) {
+        const uint32_t old =
+            __hip_atomic_fetch_add(&s_svc[b % kSvcRing].done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old + k == count) svc_complete(host, b);
+    }
+}
+
+template <int KEYSEL, int TAB>
+__global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__restrict__ tab,
+                                                         const uint32_t *__restrict__ ttab_img, SvcShared *host,
+                                                         uint32_t inf_off, uint32_t hf_off,
+                                                         uint64_t idle_ticks)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    UniformKey ukey(tab);
+    if (threadIdx.x == 0) {
+        s_svc_next = 0;
+        s_svc_loaded = 0;
+        s_svc_lock = 0;
+    }
+    fill_ttab_dma_issue<TAB, 1024>(ttab_img);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
+    __syncthreads();
+    const Lane l = lane_bases();
+    // KEYSEL_ZERO with slot 0 empty: every packet fails closed (xdp.c:83-84)
+    const bool keyok = KEYSEL == HFV_KEYSEL_IFID || ukey.ok;
+    const UniformKey *ukp = KEYSEL == HFV_KEYSEL_ZERO ? &ukey : nullptr;
+
+    uint32_t mb = 0;
+    SvcTile cur, none;
+    none.base = 0;
+    none.count = 0;
+    uint32_t g = 0;
+    if (lane == 0) g = __hip_atomic_fetch_add(&s_svc_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (svc_map(host, idle_ticks, lane, wave_uniform(g), true, mb, none, cur) != kSvcFound) return;
+    uint32_t pending = 0;   // verified tiles of cur.b not counted yet
+    // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
+    // out as ONE scattered write-through store when the wave leaves the batch or the stash
+    // is full.  A store per tile would sit in the wave's in-order vmcnt queue in front of
+    // the next tile's record loads and expose its (memory-side) acknowledge every tile.
+    uint64_t st_word = 0, st_tile = 0;
+    uint32_t stashed = 0;
+    auto load = [&](const SvcTile &t) {
+        if constexpr (HFV_SVC_ACQ == 2)
+            return load_rec_sys((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
+        else
+            return load_rec((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
+    };
+    RecWords rc = load(cur);
+    svc_prefetch(host, idle_ticks, lane, cur.b);
+    for (;;) {
+        // claim and prefetch the next tile before computing this one; a claim in a batch
+        // the host has not posted yet is resolved after this tile is counted, so a host
+        // that waits for this batch before posting the next never waits on us
+        g = 0;
+        if (lane == 0) g = __hip_atomic_fetch_add(&s_svc_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        g = wave_uniform(g);
+        SvcTile nx;
+        SvcClaim c = svc_map(host, idle_ticks, lane, g, false, mb, cur, nx);
+        if (c != kSvcFound) nx = cur;
+        RecWords rn = load(nx);
+        uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
+        if (keyok) {
+            RecWords c1[1] = {rc};
+            verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
+        }
+        if (lane == stashed) {
+            st_word = ballot;
+            st_tile = cur.tile;
+        }
+        ++stashed;
+        ++pending;
+        const bool leave = c != kSvcFound || nx.b != cur.b;
+        if (leave || stashed == 64) {
+            if (lane < stashed)
+                __hip_atomic_store(reinterpret_cast<uint64_t *>(cur.bits) + st_tile, st_word, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            stashed = 0;
+        }
+        if (leave) {
+            svc_count(host, lane, cur.b, cur.count, pending);
+            pending = 0;
+        }
+        if (c == kSvcPending) {
+            c = svc_map(host, idle_ticks, lane, g, true, mb, none, nx);
+            if (c == kSvcFound) rn = load(nx);
+        }
+        if (c == kSvcStop) break;
+        if (nx.b != cur.b) svc_prefetch(host, idle_ticks, lane, nx.b);
+        cur = nx;
+        rc = rn;
+    }
+}
+
+int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, uint32_t inf_off,
+                          uint32_t hf_off, uint64_t idle_ticks, void *stream, void *ev_start, void *ev_stop,
+                          unsigned *grid_out)
+{
+    auto k = keysel == HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_IFID, 2> : k_verify_service<HFV_KEYSEL_ZERO, 4>;
+    const char *ge = getenv("HFV_SVC_GRID");   // experiments only: fewer blocks than CUs
+    unsigned grid = ge && atoi(ge) > 0 && atoi(ge) < g.num_cus ? (unsigned)atoi(ge) : (unsigned)g.num_cus;
+    if (grid > kSvcMaxBlocks) grid = kSvcMaxBlocks;
+    *grid_out = grid;
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, host, inf_off, hf_off,
+                          idle_ticks);
+    return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------

@@ -84,6 +84,12 @@ def lib():
         "hfv_host_unregister": (i32, [vp, vp]),
         "hfv_cmac_tags": (i32, [vp, vp, vp, sz, vp, vp]),
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
+        "hfv_service_start": (i32, [vp, u32]),
+        "hfv_service_submit": (i32, [vp, vp, sz, sz, vp, ctypes.POINTER(u64)]),
+        "hfv_service_poll": (i32, [vp, u64]),
+        "hfv_service_wait": (i32, [vp, u64, i32]),
+        "hfv_service_stop": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "hfv_service_running": (i32, [vp]),
         "hfv_expand_keys": (i32, [vp, vp, sz, vp, vp]),
         "hfv_gen_records": (i32, [vp, vp, sz, sz, u64, u64, vp]),
         "hfv_verify_macinput": (i32, [vp, u64, vp]),
@@ -306,6 +312,35 @@ class Ctx:
 
     def gen_records(self, recs, n, seed, first_index=0, stride=REC_SIZE, stream=None):
         _check(lib().hfv_gen_records(self._h, _ptr(recs), stride, n, seed, first_index, _stream(stream)))
+
+    # resident verify service (persistent grid fed through a host descriptor ring)
+    def service_start(self, idle_ms=0):
+        _check(lib().hfv_service_start(self._h, idle_ms))
+
+    def service_submit(self, recs, n, pass_bits, stride=REC_SIZE):
+        """Post one batch (device buffers); returns its ticket."""
+        t = ctypes.c_uint64()
+        _check(lib().hfv_service_submit(self._h, _ptr(recs), stride, n, _ptr(pass_bits), ctypes.byref(t)))
+        return t.value
+
+    def service_poll(self, ticket):
+        rc = lib().hfv_service_poll(self._h, ticket)
+        if rc < 0:
+            _check(rc)
+        return bool(rc)
+
+    def service_wait(self, ticket, timeout_ms=-1):
+        _check(lib().hfv_service_wait(self._h, ticket, timeout_ms))
+
+    def service_stop(self):
+        """Finish posted batches, stop the grid; returns its lifetime in ms."""
+        ms = ctypes.c_float(0.0)
+        _check(lib().hfv_service_stop(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    @property
+    def service_running(self):
+        return bool(lib().hfv_service_running(self._h))
 
     # host buffers (pinned staging, H2D/kernel/D2H overlapped)
     def verify_records_host(self, recs, n, pass_bits, stride=REC_SIZE):

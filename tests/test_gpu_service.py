@@ -1,0 +1,214 @@
+"""Parity of the resident verify service (hfv_service_*: persistent grid fed through the host
+descriptor ring) against the CPU checker, the committed fixtures and the launch-per-batch
+path.  Integer work: every comparison is bit-exact.
+
+hfv_service_submit is host-ordered, not stream-ordered: a batch's records and bitmap must be
+complete when it is posted, so the tests synchronize torch's stream after preparing them."""
+import time
+
+import numpy as np
+import pytest
+
+import orc
+import scion_hfv as hfv
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def dev(a):
+    return torch.from_numpy(np.array(a, copy=True)).to(DEV)
+
+
+def new_bits(n, fill=0):
+    return torch.full((max(1, (n + 63) // 64),), fill, dtype=torch.int64, device=DEV)
+
+
+def bits_np(t, n):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64)[: (n + 63) // 64]
+
+
+@pytest.fixture()
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = hfv.Ctx(0)
+    yield c
+    c.service_stop()
+    c.close()
+
+
+@pytest.mark.parametrize("name,keysel", [("hf_single.npz", 0), ("hf_ifid256.npz", 1)])
+def test_service_golden(ctx, name, keysel):
+    g = orc.load_golden(name)
+    n = len(g["records"])
+    raw = g["raw_keys"].reshape(-1).tobytes()
+    for k in range(int(g["nkeys"])):
+        ctx.key_add(k, raw[16 * k:16 * k + 16])
+    ctx.set_keysel(keysel)
+    bits = new_bits(n, fill=-1)
+    d = dev(g["records"])
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, bits)
+    ctx.service_wait(t, 20000)
+    assert ctx.service_poll(t)
+    assert np.array_equal(bits_np(bits, n), g["pass_bits"])
+    ms = ctx.service_stop()
+    assert ms > 0 and not ctx.service_running
+
+
+@pytest.mark.parametrize("keysel", [0, 1])
+def test_service_ragged_batches_vs_oracle(ctx, keysel):
+    """Many batches of ragged sizes (incl. 0, 1 and sizes smaller than the grid, where most
+    blocks own no tile) in flight at once, each against the oracle."""
+    rng = np.random.default_rng(21 + keysel)
+    raw = orc.gen_key_table(256)
+    hk, valid = orc.key_table(raw)
+    for k in range(256):
+        ctx.key_add(k, raw[16 * k:16 * k + 16])
+    ctx.set_keysel(keysel)
+    recs = orc.gen_records(41000, hk, keysel, seed=77)   # offsets < 1000 + sizes <= 40000
+    junk = rng.random(len(recs)) < 0.2
+    recs[junk] = rng.integers(0, 256, size=(int(junk.sum()), 64), dtype=np.uint8)
+    d = dev(recs)
+    sizes = [0, 1, 2, 63, 64, 65, 127, 255, 4097, 16385, 40000] * 9   # 99 batches > 64-slot ring
+    bufs = [new_bits(n, fill=-1) for n in sizes]
+    torch.cuda.synchronize()
+    outs = []
+    for i, (n, b) in enumerate(zip(sizes, bufs)):
+        off = (i * 977) % 1000
+        t = ctx.service_submit(d[off:], n, b)
+        outs.append((t, off, n, b))
+    for t, off, n, b in outs:
+        ctx.service_wait(t, 20000)
+    for t, off, n, b in outs:
+        if n == 0:
+            continue
+        want = orc.verify_records(recs[off:off + n], hk, valid, keysel)
+        got = bits_np(b, n)
+        bad = np.nonzero(got != want)[0]
+        assert not len(bad), (t, off, n, bad[:8], got[bad[:4]], want[bad[:4]])
+
+
+def test_service_matches_launch_path_full_size(ctx):
+    """2^20 and 2^24 records: service verdicts == launch-path verdicts == generator truth."""
+    ctx.key_add(0, orc.KEY_1111)
+    for n in (1 << 20, 1 << 24):
+        recs = torch.empty((n, 64), dtype=torch.uint8, device=DEV)
+        ctx.gen_records(recs, n, orc.SEED_RECORDS)
+        a = new_bits(n)
+        ctx.verify_records(recs, n, a)
+        b = new_bits(n, fill=-1)
+        torch.cuda.synchronize()
+        tickets = [ctx.service_submit(recs, n, b) for _ in range(3)]
+        ctx.service_wait(tickets[-1], 20000)
+        assert torch.equal(a, b)
+        got = hfv.bits_to_bool(bits_np(b, n), n)
+        assert np.array_equal(got, orc.expected_pass_rule(n))
+        ctx.service_stop()
+        del recs
+
+
+def test_service_sees_rewritten_records(ctx):
+    """A batch buffer rewritten between batches (as an RX ring is) is read fresh: the grid
+    drops stale cache lines when it picks up a descriptor."""
+    ctx.key_add(0, orc.KEY_1111)
+    hk, valid = orc.key_table(orc.KEY_1111)
+    n = 200_000
+    a = orc.gen_records(n, hk, 0, seed=1)
+    b = orc.gen_records(n, hk, 0, seed=2)
+    d = dev(a)
+    bits = new_bits(n)
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, bits)
+    ctx.service_wait(t, 20000)
+    assert np.array_equal(bits_np(bits, n), orc.verify_records(a, hk, valid, 0))
+    d.copy_(torch.from_numpy(b).to(DEV))
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, bits)
+    ctx.service_wait(t, 20000)
+    assert np.array_equal(bits_np(bits, n), orc.verify_records(b, hk, valid, 0))
+
+
+def test_service_key_change_is_a_batch_boundary(ctx):
+    """Key add/remove while the service runs apply from the next submitted batch on; the
+    batches posted before keep the old table."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    outs = [new_bits(n, fill=-1) for _ in range(3)]
+    torch.cuda.synchronize()
+    t0 = ctx.service_submit(d, n, outs[0])
+    ctx.key_remove(0)
+    t1 = ctx.service_submit(d, n, outs[1])
+    ctx.key_add(0, orc.KEY_1111)
+    t2 = ctx.service_submit(d, n, outs[2])
+    for t in (t0, t1, t2):
+        ctx.service_wait(t, 20000)
+    assert np.array_equal(bits_np(outs[0], n), g["pass_bits"])
+    assert not bits_np(outs[1], n).any()            # slot 0 empty: fail closed
+    assert np.array_equal(bits_np(outs[2], n), g["pass_bits"])
+
+
+def test_service_no_key_fails_closed(ctx):
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    bits = new_bits(n, fill=-1)
+    d = dev(g["records"])
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, bits)
+    ctx.service_wait(t, 20000)
+    assert not bits_np(bits, n).any()
+
+
+def test_service_coexists_with_launch_path(ctx):
+    """A launch-path call stops the service at a batch boundary; the next submit restarts it."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    b1, b2, b3 = new_bits(n, -1), new_bits(n, -1), new_bits(n, -1)
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, b1)
+    ctx.verify_records(d, n, b2)
+    assert not ctx.service_running
+    ctx.service_wait(t, 1000)                      # completed before the stop
+    t = ctx.service_submit(d, n, b3)
+    assert ctx.service_running
+    ctx.service_wait(t, 20000)
+    for b in (b1, b2, b3):
+        assert np.array_equal(bits_np(b, n), g["pass_bits"])
+
+
+def test_service_idle_exit_and_restart(ctx):
+    """The grid leaves by itself after idle_ms without work; the next submit starts a new one."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    ctx.service_start(idle_ms=50)
+    b = new_bits(n, -1)
+    b2 = new_bits(n, -1)
+    torch.cuda.synchronize()
+    t = ctx.service_submit(d, n, b)
+    ctx.service_wait(t, 20000)
+    time.sleep(0.5)                                # > idle_ms: the grid has exited
+    t = ctx.service_submit(d, n, b2)               # restarts it
+    ctx.service_wait(t, 20000)
+    assert np.array_equal(bits_np(b2, n), g["pass_bits"])
+
+
+def test_service_bad_arguments(ctx):
+    ctx.key_add(0, orc.KEY_1111)
+    bits = new_bits(4)
+    recs = torch.zeros((4, 64), dtype=torch.uint8, device=DEV)
+    with pytest.raises(hfv.HfvError):
+        ctx.service_submit(recs.data_ptr() + 4, 3, bits)
+    with pytest.raises(hfv.HfvError):
+        ctx.service_submit(recs, 4, bits, stride=40)
+    with pytest.raises(hfv.HfvError):
+        ctx.service_wait(12345)

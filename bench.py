@@ -8,10 +8,11 @@ records (BASELINE.json metric; config 2 = 2^20 records, single AS key, per GPU).
 One process per GPU.  A "step" is one pass of the verifier over the rank's resident batch
 of n records (weak scaling: every rank verifies its own n records, no collective on the
 data path; RCCL is used only for the timing barrier and max-over-ranks).  By default
-(--mode launch) a step is one hfv_verify_records launch; --mode service posts the K
-batches one by one to the resident service (hfv_service_submit) with starting and
-stopping its grid inside the timed region (both are always measured and reported:
-`per_launch`, `service`).  Rank 0 prints one JSON line.  Besides
+(--mode service) the K steps are K batches posted one by one to the resident service
+(hfv_service_submit: the XDP program's counterpart, a grid that stays on the GPU), with
+starting and stopping its grid inside the timed region; --mode launch times one
+hfv_verify_records launch per step instead (both are always measured and reported:
+`service`, `per_launch`).  Rank 0 prints one JSON line.  Besides
 the contract fields it carries:
   roofline      -- the headline kernel's algorithmic bytes (64 B read + 1/8 B verdict per
                    record) / its duration from the dispatch's own start/stop events (the
@@ -126,12 +127,13 @@ def timed_steps(world, steps, fn):
     return elapsed
 
 
-def pmc_traffic(keysel, n):
-    """HBM bytes per launch measured by rocprofv3 PMC passes (scripts/pmc_round.sh) for this
-    exact configuration, committed in profiles/traffic.json; None if not measured."""
+def pmc_traffic(keysel, n, service=False):
+    """HBM bytes per launch (per batch for the resident service) measured by rocprofv3 PMC
+    passes (scripts/pmc_round.sh) for this exact configuration, committed in
+    profiles/traffic.json; None if not measured."""
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        return json.load(open(tpath))[f"{keysel}:{n}"]["hbm_bytes_per_launch"]
+        return json.load(open(tpath))[f"{'svc:' if service else ''}{keysel}:{n}"]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -410,7 +412,7 @@ def main():
     ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
                     help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
                          "br-host: config 5")
-    ap.add_argument("--mode", choices=["service", "launch"], default="launch",
+    ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")
     ap.add_argument("--no-register", action="store_true", help="br-host: leave the ring unregistered (DMA windows)")
@@ -490,7 +492,7 @@ def main():
     service = {"mpkts": round(world * n * args.steps / svc_elapsed / 1e6, 2),
                "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4)}
 
-    traffic = pmc_traffic(args.keysel, n)
+    traffic = pmc_traffic(args.keysel, n, service=headline == "service")
 
     result = {
         "metric": "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets",

@@ -183,6 +183,7 @@ struct hfv_ctx {
     hipStream_t svc_stream = nullptr;
     SvcShared *svc_host = nullptr;   // descriptor ring + completions, coherent pinned memory
     SvcShared *svc_host_dev = nullptr;
+    SvcDesc *svc_mirror = nullptr;   // device copy of the descriptor ring (the grid's relay writes it)
     unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
     uint64_t svc_next = 1;           // next ticket
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
@@ -326,6 +327,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         (void)hipStreamDestroy(ctx->svc_stream);
     }
     if (ctx->svc_host) (void)hipHostFree(ctx->svc_host);
+    if (ctx->svc_mirror) (void)hipFree(ctx->svc_mirror);
     for (int i = 0; i < 2; ++i)
         if (ctx->svc_ev[i]) (void)hipEventDestroy(ctx->svc_ev[i]);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -1141,9 +1143,12 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
         HIP_TRY(hipHostMalloc((void **)&ctx->svc_host, sizeof(SvcShared),
                               hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&ctx->svc_host_dev, ctx->svc_host, 0));
+        HIP_TRY(hipMalloc((void **)&ctx->svc_mirror, kSvcRing * sizeof(SvcDesc)));
         for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreate(&ctx->svc_ev[i]));
     }
     memset(ctx->svc_host, 0, sizeof(SvcShared));
+    // stale tickets of an earlier run must not match: the mirror starts empty
+    HIP_TRY(hipMemsetAsync(ctx->svc_mirror, 0, kSvcRing * sizeof(SvcDesc), ctx->svc_stream));
     DevState *ds;
     int rc = publish_keys(ctx, ctx->svc_stream, &ds);
     if (rc) return rc;
@@ -1152,7 +1157,7 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     ctx->svc_hf_off = ctx->hf_off;
     ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
     ctx->svc_next = 1;
-    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->inf_off, ctx->hf_off,
+    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off, ctx->hf_off,
                                   (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_stream, ctx->svc_ev[0],
                                   ctx->svc_ev[1], &ctx->svc_grid);
     rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");

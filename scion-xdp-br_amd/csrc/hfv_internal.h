@@ -75,7 +75,9 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out);
 enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 
 // Resident verify service (hfv_service_*): the host posts batch descriptors into a ring in
-// pinned, coherent host memory; the persistent grid polls it, verifies each batch, and every
+// pinned, coherent host memory; one wave of the persistent grid copies each posted
+// descriptor into a device-memory mirror (SvcDesc[kSvcRing]) that every block polls instead
+// of reaching over PCIe; the grid verifies each batch, and every
 // block publishes the completion of its share of a batch straight into host memory (one
 // posted PCIe write; the host combines the per-block flags).  Batch b (0-based, ticket b+1)
 // uses ring slot b % kSvcRing; the host posts ticket t only once ticket t - kSvcRing is
@@ -138,7 +140,8 @@ int build_ttab_image(uint32_t *img, void *stream);
 // persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
 // block waits for the next descriptor before it exits with status kSvcIdleTimeout
 // returns the grid size in *grid
-int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, uint32_t inf_off,
+int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
+                          uint32_t inf_off,
                           uint32_t hf_off, uint64_t idle_ticks, void *stream, void *ev_start, void *ev_stop,
                           unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)

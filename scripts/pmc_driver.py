@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Workload for rocprofv3 --pmc passes: verify 2^20 and 2^24 records (config 2, and config 3
-with --keysel ifid), `reps` launches each, after one untimed generation pass."""
+with --keysel ifid), `reps` launches each, after one untimed generation pass.  With a 4th
+argument `svc` the batches go through the resident service instead: per size one 2-batch
+grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches."""
 import os
 import sys
 
@@ -42,6 +44,7 @@ def main():
         return run_br(int(sys.argv[2]) if len(sys.argv) > 2 else 10)
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
+    svc = len(sys.argv) > 4 and sys.argv[4] == "svc"
     torch.cuda.set_device(0)
     ctx = hfv.Ctx(0)
     if keysel == "ifid":
@@ -53,8 +56,16 @@ def main():
         recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
         bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
         ctx.gen_records(recs, n, SEED_RECORDS)
-        for _ in range(reps):
-            ctx.verify_records(recs, n, bits)
+        if svc:
+            torch.cuda.synchronize()
+            for k in (2, reps):
+                ctx.service_start()
+                for _ in range(k):
+                    ctx.service_submit(recs, n, bits)
+                ctx.service_stop()
+        else:
+            for _ in range(reps):
+                ctx.verify_records(recs, n, bits)
         torch.cuda.synchronize()
         del recs, bits
     ctx.close()

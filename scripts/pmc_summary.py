@@ -11,7 +11,8 @@ import sys
 from collections import defaultdict
 
 
-def main(d, sizes, kernel="k_verify_records"):
+def main(d, sizes, kernel="k_verify_records", per=1):
+    """per: batches per dispatch (the resident service runs `per` batches in one grid)."""
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         disp = defaultdict(lambda: {"name": "", "c": defaultdict(float)})
@@ -38,7 +39,7 @@ def main(d, sizes, kernel="k_verify_records"):
                 acc[label][c].append(v)
     out = {}
     for label, cs in acc.items():
-        o = {c: sum(v) / len(v) for c, v in cs.items()}
+        o = {c: sum(v) / len(v) / per for c, v in cs.items()}
         if "FETCH_SIZE" in o:
             o["hbm_read_bytes_per_launch"] = o["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in o:
@@ -52,4 +53,4 @@ def main(d, sizes, kernel="k_verify_records"):
 
 if __name__ == "__main__":
     main(sys.argv[1], [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1048576,16777216").split(",")],
-         sys.argv[3] if len(sys.argv) > 3 else "k_verify_records")
+         sys.argv[3] if len(sys.argv) > 3 else "k_verify_records", int(sys.argv[4]) if len(sys.argv) > 4 else 1)

@@ -546,7 +546,8 @@ def main():
                                   "traffic": pmc_traffic(args.keysel, nb),
                                   "service_ms_per_batch": round(sg / 10, 4),
                                   "service_mpkts": round(nb * 10 / sg / 1e3, 1),
-                                  "service_frac": round(sach / HBM_PEAK_GBS, 4)}
+                                  "service_frac": round(sach / HBM_PEAK_GBS, 4),
+                                  "service_traffic": pmc_traffic(args.keysel, nb, service=True)}
         del big, bbits
 
     if rank == 0 and world == 1 and not args.no_host_e2e:

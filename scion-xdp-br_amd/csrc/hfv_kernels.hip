@@ -226,13 +226,28 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
         }
         ukp = &ukey;
     }
+    // Verdict words wait in a per-wave stash (lane j: the wave's j-th tile) and go out as one
+    // store per 64 tiles: a store per tile sits in the in-order vmcnt queue, and the loop
+    // latch (which waits for the prefetched record words) would wait for its write
+    // acknowledgement every tile.
+    uint64_t st_word = 0;
+    uint32_t st_tile = 0, stashed = 0;
     while (t < count) {
         uint32_t nt = 0;
         if (lane == 0) nt = atomicAdd(&s_next_tile, 1u);
         nt = wave_uniform(nt);
         RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
         RecWords c1[1] = {cur};
-        verify_tiles<KEYSEL, TAB, 1>(c1, b0 + t, 0, n, lane, l, ukp, bits);
+        uint64_t ballot;
+        verify_tiles<KEYSEL, TAB, 1, 1>(c1, b0 + t, 0, n, lane, l, ukp, nullptr, &ballot);
+        if (lane == stashed) {
+            st_word = ballot;
+            st_tile = t;
+        }
+        if (++stashed == 64) {
+            ((GlobalU64 *)bits)[b0 + st_tile] = st_word;
+            stashed = 0;
+        }
         if constexpr (STAMP) {
             if (lane == 0 && nst < 10) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
             ++nst;
@@ -240,6 +255,7 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
         cur = nxt;
         t = nt;
     }
+    if (lane < stashed) ((GlobalU64 *)bits)[b0 + st_tile] = st_word;
     if constexpr (STAMP) {
         if (lane == 0) {
             st[13] = __builtin_amdgcn_s_memtime();
@@ -890,6 +906,11 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     RecWords rc = load(cur);
     svc_prefetch(host, mir, idle_ticks, lane, cur.b);
     for (;;) {
+        // This tile's record words are complete before the next tile's loads are issued:
+        // without this explicit wait (a builtin, so the waitcnt pass sees it) the pass merges
+        // the loop's several entry paths and puts a vmcnt(0) AFTER the next tile's loads, in
+        // front of this tile's rounds, which serialises load latency and compute per tile.
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
         // claim and prefetch the next tile before computing this one; a claim in a batch
         // the host has not posted yet is resolved after this tile is counted, so a host
         // that waits for this batch before posting the next never waits on us

@@ -127,6 +127,24 @@ def timed_steps(world, steps, fn):
     return elapsed
 
 
+def ceilings(keysel):
+    """The other bounds beside HBM, per packet, from this repo's own measurements (DESIGN.md
+    section 4): LDS lookups and VALU instructions per packet (PMC SQ_INSTS_LDS/VALU x 64 /
+    records, profiles/r01/service/pmc_zero_svc), the chip's conflict-free ds_read_b32 rate
+    (scripts/ubench/valu_rate.hip) and the streaming-read rate of the same access pattern
+    without compute (scripts/ubench/stream_read.hip, 1 GiB)."""
+    lds_per_pkt = 146.2 if keysel == "zero" else None
+    lds_rate = 16.8e12
+    out = {"lds_lookups_per_pkt": lds_per_pkt, "lds_peak_lookups_per_s": lds_rate,
+           "valu_instr_per_pkt": 277.0 if keysel == "zero" else None,
+           "streaming_read_GBs": 6552.0, "streaming_read_frac": round(6552.0 / HBM_PEAK_GBS, 3),
+           "source": "profiles/r01/service/pmc_zero_svc/summary.json, profiles/r01/ubench/"}
+    if lds_per_pkt:
+        out["lds_bound_mpkts"] = round(lds_rate / lds_per_pkt / 1e6, 1)
+    out["streaming_read_bound_mpkts"] = round(6552.0e9 / hfv.BYTES_PER_PACKET / 1e6, 1)
+    return out
+
+
 def pmc_traffic(keysel, n, service=False):
     """HBM bytes per launch (per batch for the resident service) measured by rocprofv3 PMC
     passes (scripts/pmc_round.sh) for this exact configuration, committed in
@@ -515,6 +533,7 @@ def main():
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}, **kern,
                          variant=ctx.describe(),
                          note="2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"),
+        "ceilings": ceilings(args.keysel),
         "path": ("resident service: one persistent grid, the K batches posted one by one through the host "
                  "descriptor ring (hfv_service_submit); grid launch, table fill and drain inside the timed region"
                  if headline == "service" else "one hfv_verify_records launch per batch"),

@@ -145,6 +145,17 @@ def ceilings(keysel):
     return out
 
 
+def lds_bound_at_clock(keysel, mhz):
+    """The LDS-issue bound at the shader clock the service grid actually ran at (it is power
+    limited: ~2.38 GHz with 32 CUs busy, ~1.5-1.6 GHz sustained with all 256, scripts/svc_probe.py):
+    conflict-free ds_read_b32 retires 32 lanes per clock per CU."""
+    if not mhz or keysel != "zero":
+        return {}
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    return {"service_shader_mhz": round(mhz, 1),
+            "lds_bound_mpkts_at_service_clock": round(cus * 32 * mhz * 1e6 / 146.2 / 1e6, 1)}
+
+
 def pmc_traffic(keysel, n, service=False):
     """HBM bytes per launch (per batch for the resident service) measured by rocprofv3 PMC
     passes (scripts/pmc_round.sh) for this exact configuration, committed in
@@ -484,6 +495,7 @@ def main():
         for _ in range(args.steps):
             ctx.service_submit(recs, n, bits)
         svc["grid_ms"] = ctx.service_stop()
+        svc["shader_mhz"] = ctx.service_shader_mhz()
 
     svc_elapsed = timed_steps(world, 1, service_run)
     assert popcount(bits) == expected_pass_count(n, rank * n)
@@ -508,7 +520,8 @@ def main():
                   "kernel_mpkts": round(n / k_mean / 1e3, 1),
                   "frac": round(bytes_per_launch / (k_mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     service = {"mpkts": round(world * n * args.steps / svc_elapsed / 1e6, 2),
-               "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4)}
+               "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4),
+               "shader_mhz": round(svc["shader_mhz"], 1) if svc["shader_mhz"] else None}
 
     traffic = pmc_traffic(args.keysel, n, service=headline == "service")
 
@@ -533,7 +546,7 @@ def main():
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}, **kern,
                          variant=ctx.describe(),
                          note="2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"),
-        "ceilings": ceilings(args.keysel),
+        "ceilings": dict(ceilings(args.keysel), **lds_bound_at_clock(args.keysel, svc["shader_mhz"])),
         "path": ("resident service: one persistent grid, the K batches posted one by one through the host "
                  "descriptor ring (hfv_service_submit); grid launch, table fill and drain inside the timed region"
                  if headline == "service" else "one hfv_verify_records launch per batch"),
@@ -558,6 +571,7 @@ def main():
         for _ in range(10):
             ctx.service_submit(big, nb, bbits)
         sg = ctx.service_stop()
+        smhz = ctx.service_shader_mhz()
         assert popcount(bbits) == expected_pass_count(nb, 0)
         sach = hfv.BYTES_PER_PACKET * nb * 10 / (sg * 1e-3) / 1e9
         result["hbm_resident"] = {"records": nb, "kernel_ms_mean": round(bm, 4), "mpkts": round(nb / bm / 1e3, 1),
@@ -566,7 +580,8 @@ def main():
                                   "service_ms_per_batch": round(sg / 10, 4),
                                   "service_mpkts": round(nb * 10 / sg / 1e3, 1),
                                   "service_frac": round(sach / HBM_PEAK_GBS, 4),
-                                  "service_traffic": pmc_traffic(args.keysel, nb, service=True)}
+                                  "service_traffic": pmc_traffic(args.keysel, nb, service=True),
+                                  "service_shader_mhz": round(smhz, 1) if smhz else None}
         del big, bbits
 
     if rank == 0 and world == 1 and not args.no_host_e2e:

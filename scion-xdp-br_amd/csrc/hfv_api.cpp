@@ -1223,11 +1223,13 @@ int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms)
 int hfv_service_running(const hfv_ctx *ctx) { return ctx && ctx->svc_running ? 1 : 0; }
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
-// 0 loaded ring slot i's descriptor.
+// 0 loaded ring slot i's descriptor; out[64..67] = block 0 wave 0's s_memtime and
+// s_memrealtime at its start and at its exit (the shader clock over the grid's life).
 int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
 {
     if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
     for (uint32_t i = 0; i < kSvcRing; ++i) out[i] = __atomic_load_n(&ctx->svc_host->load_clock[i], __ATOMIC_ACQUIRE);
+    for (uint32_t i = 0; i < 4; ++i) out[kSvcRing + i] = __atomic_load_n(&ctx->svc_host->run_clock[i], __ATOMIC_ACQUIRE);
     return 0;
 }
 

@@ -96,6 +96,7 @@ struct SvcShared {
     uint64_t status;                 // nonzero: the grid stopped on its own (kSvcIdleTimeout, kSvcWatchdog)
     uint64_t pad[7];
     uint64_t load_clock[kSvcRing];   // diagnostics: s_memrealtime when block 0 loaded the slot
+    uint64_t run_clock[4];           // diagnostics: block 0 wave 0 s_memtime/s_memrealtime at start, at exit
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;

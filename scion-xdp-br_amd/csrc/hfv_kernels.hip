@@ -882,6 +882,11 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     const bool keyok = KEYSEL == HFV_KEYSEL_IFID || ukey.ok;
     const UniformKey *ukp = KEYSEL == HFV_KEYSEL_ZERO ? &ukey : nullptr;
 
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // diagnostics: shader clock over the grid's life
+        __hip_atomic_store(&host->run_clock[0], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host->run_clock[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     uint32_t mb = 0;
     SvcTile cur, none;
     none.base = 0;
@@ -951,6 +956,11 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if (nx.b != cur.b) svc_prefetch(host, mir, idle_ticks, lane, nx.b);
         cur = nx;
         rc = rn;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&host->run_clock[2], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host->run_clock[3], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -338,6 +338,17 @@ class Ctx:
         _check(lib().hfv_service_stop(self._h, ctypes.byref(ms)))
         return ms.value
 
+    def service_shader_mhz(self):
+        """Diagnostic: block 0's shader clock over the last service grid's life (s_memtime
+        against the 100 MHz s_memrealtime), or None."""
+        clk = (ctypes.c_uint64 * 68)()
+        L = lib()
+        L.hfv_debug_service_clocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        if L.hfv_debug_service_clocks(self._h, clk) != 0:
+            return None
+        t0, r0, t1, r1 = (int(x) for x in clk[64:68])
+        return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
+
     @property
     def service_running(self):
         return bool(lib().hfv_service_running(self._h))

@@ -35,13 +35,16 @@ for rep in range(3):
     for t in tickets:
         ctx.service_wait(t, 20000)
         done.append(time.perf_counter() - t0)
-    clk = np.zeros(64, dtype=np.uint64)
+    clk = np.zeros(68, dtype=np.uint64)
     L.hfv_debug_service_clocks(ctx._h, clk.ctypes.data)
     grid = ctx.service_stop()
+    L.hfv_debug_service_clocks(ctx._h, clk.ctypes.data)   # exit stamps are written at stop
+    rc = [int(x) for x in clk[64:68]]
+    shader_mhz = (rc[2] - rc[0]) / ((rc[3] - rc[1]) / 100.0) if rc[3] > rc[1] else None
     done_us = np.array(done) * 1e6
     gaps = np.diff(done_us)
     ld = (clk[:K].astype(np.int64) - int(clk[0])) / 100.0
-    print(json.dumps({"n": n, "K": K, "grid_ms": round(grid, 4), "host_done_ms": round(done[-1] * 1e3, 3),
+    print(json.dumps({"n": n, "K": K, "grid_ms": round(grid, 4), "shader_mhz": round(shader_mhz, 1) if shader_mhz else None, "host_done_ms": round(done[-1] * 1e3, 3),
                       "post_loop_ms": round(posts[-1] * 1e3, 3), "post_us_mean": round(posts[-1] / K * 1e6, 2),
                       "done_gap_us_median": round(float(np.median(gaps)), 2),
                       "done_gap_us_p10_p90": [round(float(np.percentile(gaps, 10)), 2),

@@ -975,7 +975,7 @@ static int verify_records_zero_copy(hfv_ctx *ctx, const uint8_t *drecs, size_t s
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
     int e = launch_verify_records(ctx->geom, &ds->keys, ctx->keysel, drecs, stride, n, ctx->inf_off, ctx->hf_off,
-                                  dbits, st);
+                                  dbits, st, nullptr, nullptr, /*interleaved=*/true);
     rc = after_launch(ctx, st, e, "verify_records launch (zero-copy)");
     if (rc) return rc;
     if (dbits == (uint64_t *)ctx->zc_meta) HIP_TRY(hipMemcpyAsync(pass_bits, dbits, words * 8, hipMemcpyDeviceToHost, st));

@@ -1205,9 +1205,10 @@ static VerifyKernel pick_verify(const KernelVariant &v)
 
 int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream,
-                          void *ev_start, void *ev_stop)
+                          void *ev_start, void *ev_stop, bool interleaved)
 {
-    const KernelVariant &v = keysel == HFV_KEYSEL_IFID ? g.multi : g.single;
+    KernelVariant v = keysel == HFV_KEYSEL_IFID ? g.multi : g.single;
+    if (interleaved && v.bs == 0) v.dyn = 0;   // the static kernel walks the tiles grid-stride
     VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(v) : pick_verify<HFV_KEYSEL_ZERO>(v);
     if (!k) return (int)hipErrorInvalidConfiguration;
     unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);

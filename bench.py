@@ -595,7 +595,8 @@ def main():
         th = (time.perf_counter() - t0) / reps
         assert np.array_equal(hbits, bits.cpu().numpy().view(np.uint64))
         result["host_e2e"] = {"mpkts": round(n / th / 1e6, 1), "ms_per_batch": round(th * 1e3, 3),
-                              "path": "pageable host -> pinned -> H2D -> kernel -> D2H -> host, 2 streams"}
+                              "path": "pageable host -> INF/HF gathered into 24 B pinned staging records (host threads) -> H2D -> "
+                                      "kernel -> D2H -> host, 2^18-record chunks on 2 streams"}
         # the same batch in a registered (pinned, mapped) ring: the kernel reads the records'
         # INF/HF words across PCIe in place and writes the registered bitmap in place
         ring = hfv.host_array((n, hfv.REC_SIZE), np.uint8)
@@ -612,8 +613,8 @@ def main():
         ctx.host_unregister(ring)
         ctx.host_unregister(rbits)
         result["host_e2e_zero_copy"] = {"mpkts": round(n / tz / 1e6, 1), "ms_per_batch": round(tz * 1e3, 3),
-                                        "path": "registered host ring read by the kernel over PCIe (20 of 64 B per "
-                                                "record), bitmap written to registered host memory"}
+                                        "path": "registered host ring read by the kernel over PCIe in place (grid-stride "
+                                                "tiles; PCIe moves whole 64 B lines), bitmap written to registered host memory"}
 
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         result["cpu_baseline"] = cpu_baseline(recs.cpu().numpy(), keysel, bits.cpu().numpy().view(np.uint64),

@@ -13,6 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <thread>
+#include <vector>
+
 #include <hip/hip_runtime.h>
 
 #include "hfv_internal.h"
@@ -983,6 +986,51 @@ static int verify_records_zero_copy(hfv_ctx *ctx, const uint8_t *drecs, size_t s
     return 0;
 }
 
+}  // extern "C"
+
+// Compact staging record of the host path: INF (8 B) at 0, HF (12 B) at 8, 4 B pad.
+static constexpr size_t kHostRec = 24;
+
+// Host threads for the staging gather: HFV_HOST_THREADS, default min(8, cores).
+static int host_threads()
+{
+    static const int t = [] {
+        const char *e = getenv("HFV_HOST_THREADS");
+        int v = e ? atoi(e) : 0;
+        if (v <= 0) {
+            unsigned hc = std::thread::hardware_concurrency();
+            v = hc ? (int)(hc < 8 ? hc : 8) : 4;
+        }
+        return v;
+    }();
+    return t;
+}
+
+// dst[i] = {INF, HF} of src record i (the verifier's 20 bytes), split over nthreads threads.
+static void gather_hf(uint8_t *dst, const uint8_t *src, size_t stride, uint32_t inf_off, uint32_t hf_off, size_t n,
+                      int nthreads)
+{
+    auto part = [=](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            const uint8_t *r = src + i * stride;
+            uint8_t *d = dst + i * kHostRec;
+            memcpy(d, r + inf_off, 8);
+            memcpy(d + 8, r + hf_off, 12);
+        }
+    };
+    if (nthreads <= 1 || n < 8192) {
+        part(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nthreads - 1);
+    for (int k = 1; k < nthreads; ++k) th.emplace_back(part, n * k / nthreads, n * (k + 1) / nthreads);
+    part(0, n / nthreads);
+    for (auto &t : th) t.join();
+}
+
+extern "C" {
+
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
 // streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.  Records
 // in a registered buffer (hfv_host_register) take the zero-copy path instead.
@@ -998,8 +1046,12 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
     SVC_QUIESCE(ctx);
     if (const uint8_t *drecs = host_dev_ptr(ctx, recs, (n - 1) * stride + ctx->hf_off + 12))
         return verify_records_zero_copy(ctx, drecs, stride, n, pass_bits);
-    const size_t chunk = (size_t)1 << 20;   // records per chunk (64 MiB at 64 B)
-    if (ctx->host_chunk < chunk * stride) {
+    // Staging: each chunk's records are gathered on the host into a compact pinned layout of
+    // kHostRec bytes per record (INF at 0, HF at 8: the 20 bytes the verifier reads), so
+    // PCIe moves 24 B instead of the record stride; the gather is split over host threads
+    // and chunk c's gather overlaps chunk c-1's copy, kernel and copy-back on the other stream.
+    const size_t chunk = (size_t)1 << 18;   // records per chunk
+    if (ctx->host_chunk < chunk * kHostRec) {
         for (int i = 0; i < 2; ++i) {
             if (ctx->h_pin[i]) (void)hipHostFree(ctx->h_pin[i]);
             if (ctx->d_rec[i]) (void)hipFree(ctx->d_rec[i]);
@@ -1008,13 +1060,14 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
             ctx->h_pin[i] = ctx->d_rec[i] = nullptr;
             ctx->h_bits[i] = ctx->d_bits[i] = nullptr;
             if (!ctx->hstream[i]) HIP_TRY(hipStreamCreateWithFlags(&ctx->hstream[i], hipStreamNonBlocking));
-            HIP_TRY(hipHostMalloc((void **)&ctx->h_pin[i], chunk * stride, hipHostMallocDefault));
-            HIP_TRY(hipMalloc((void **)&ctx->d_rec[i], chunk * stride));
+            HIP_TRY(hipHostMalloc((void **)&ctx->h_pin[i], chunk * kHostRec, hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void **)&ctx->d_rec[i], chunk * kHostRec));
             HIP_TRY(hipHostMalloc((void **)&ctx->h_bits[i], chunk / 8, hipHostMallocDefault));
             HIP_TRY(hipMalloc((void **)&ctx->d_bits[i], chunk / 8));
         }
-        ctx->host_chunk = chunk * stride;
+        ctx->host_chunk = chunk * kHostRec;
     }
+    const int nthreads = host_threads();
     size_t nchunks = (n + chunk - 1) / chunk;
     size_t pending_words[2] = {0, 0};
     size_t pending_first[2] = {0, 0};
@@ -1027,14 +1080,15 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         }
         if (c >= nchunks) continue;
         size_t first = c * chunk, cnt = n - first < chunk ? n - first : chunk;
-        memcpy(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, cnt * stride);
-        HIP_TRY(hipMemcpyAsync(ctx->d_rec[slot], ctx->h_pin[slot], cnt * stride, hipMemcpyHostToDevice, st));
+        gather_hf(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, stride, ctx->inf_off, ctx->hf_off, cnt,
+                  nthreads);
+        HIP_TRY(hipMemcpyAsync(ctx->d_rec[slot], ctx->h_pin[slot], cnt * kHostRec, hipMemcpyHostToDevice, st));
         DevState *ds;
         int rc = publish_keys(ctx, st, &ds);
         if (rc) return rc;
         const DevKeyTable *tab = &ds->keys;
-        int e = launch_verify_records(ctx->geom, tab, ctx->keysel, ctx->d_rec[slot], stride, cnt, ctx->inf_off,
-                                      ctx->hf_off, ctx->d_bits[slot], st);
+        int e = launch_verify_records(ctx->geom, tab, ctx->keysel, ctx->d_rec[slot], kHostRec, cnt, 0, 8,
+                                      ctx->d_bits[slot], st);
         rc = after_launch(ctx, st, e, "verify_records launch");
         if (rc) return rc;
         size_t words = (cnt + 63) / 64;

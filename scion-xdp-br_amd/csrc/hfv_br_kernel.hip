@@ -60,15 +60,10 @@ __device__ __forceinline__ uint32_t sw16(uint32_t v) { return ((v & 0xffu) << 8)
 __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(v); }
 
 // Per-frame state: struct headers + the per-CPU scratchpad (common.h:154-225), zeroed per frame.
-// LDS = true: every header access goes to the frame's staged row in s_hdr (the first kBrWin
-// bytes), and a frame whose headers reach past it is `cut` before it has any effect; LDS =
-// false: every access goes to the frame in HBM.  Keeping the two apart at compile time keeps
-// HBM loads out of the staged parser, whose waits would otherwise drain the tile prefetch.
-template <bool LDS>
-struct BrFrameT {
-    static constexpr bool kLds = LDS;
+struct BrFrame {
     uint8_t *p;
-    uint32_t row;      // dword index of this frame's staged header row in s_hdr (LDS)
+    uint32_t row;      // dword index of this frame's staged header row in s_hdr
+    int win;           // staged bytes (0: read and write everything in HBM)
     bool dirty;        // the staged row was written (write it back at the end of the tile)
     int len;
     int lim;           // bytes of the frame present in the buffer (min(len, window))
@@ -94,77 +89,81 @@ struct BrFrameT {
     uint32_t mac_lo, mac_hi;
 };
 
-// Header reads (the BPF code's little-endian loads of network-order fields); a 32-bit field
-// from the staged row is two aligned ds_read_b32 + v_alignbyte.
-template <class F>
-__device__ __forceinline__ uint32_t lds_u32_at(const F &k, int off)
+// Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
+// staged window come from LDS (a 32-bit field = two aligned ds_read_b32 + v_alignbyte), the
+// rest from the frame in HBM.
+__device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
 {
     const uint32_t *row = s_hdr + k.row;
     int a = off >> 2;
     return __builtin_amdgcn_alignbyte(row[a + 1], row[a], (uint32_t)(off & 3));
 }
-template <class F>
-__device__ __forceinline__ uint32_t rd8(const F &k, int off)
+__device__ __forceinline__ uint32_t rd8(const BrFrame &k, int off)
 {
-    if constexpr (F::kLds) return reinterpret_cast<const uint8_t *>(s_hdr + k.row)[off];
-    else return g8(k.p + off);
+    if (off < k.win) return reinterpret_cast<const uint8_t *>(s_hdr + k.row)[off];
+    return g8(k.p + off);
 }
-template <class F>
-__device__ __forceinline__ uint32_t rd16(const F &k, int off)
+__device__ __forceinline__ uint32_t rd16(const BrFrame &k, int off)
 {
-    if constexpr (F::kLds) return lds_u32_at(k, off) & 0xffffu;
-    else return g16(k.p + off);
+    if (off + 2 <= k.win) return lds_u32_at(k, off) & 0xffffu;
+    return g16(k.p + off);
 }
-template <class F>
-__device__ __forceinline__ uint32_t rd32(const F &k, int off)
+__device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
 {
-    if constexpr (F::kLds) return lds_u32_at(k, off);
-    else return g32(k.p + off);
+    if (off + 4 <= k.win) return lds_u32_at(k, off);
+    return g32(k.p + off);
 }
 
-// Header writes: to the staged row (written back with coalesced 16-byte stores at the end of
-// the tile) or straight to the frame in HBM.
-template <class F>
-__device__ __forceinline__ uint8_t *wr_ptr(F &k, int off)
+// Header writes: bytes inside the staged window go to the LDS row (written back to HBM with
+// coalesced 16-byte stores at the end of the tile), bytes past it straight to HBM.
+__device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
 {
-    if constexpr (F::kLds) {
+    if (off < k.win) {
+        reinterpret_cast<uint8_t *>(s_hdr + k.row)[off] = (uint8_t)v;
         k.dirty = true;
-        return reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
     } else {
-        return k.p + off;
+        k.p[off] = (uint8_t)v;
     }
 }
-template <class F>
-__device__ __forceinline__ void wr8(F &k, int off, uint32_t v)
+__device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
 {
-    *wr_ptr(k, off) = (uint8_t)v;
+    if (off + 2 <= k.win) {   // whole field in the window (the common case): one check
+        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
+        k.dirty = true;
+    } else if (off >= k.win) {
+        k.p[off] = (uint8_t)v; k.p[off + 1] = (uint8_t)(v >> 8);
+    } else {
+        wr8(k, off, v);
+        wr8(k, off + 1, v >> 8);
+    }
 }
-template <class F>
-__device__ __forceinline__ void wr16(F &k, int off, uint32_t v)
+__device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
 {
-    uint8_t *q = wr_ptr(k, off);
-    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
-}
-template <class F>
-__device__ __forceinline__ void wr32(F &k, int off, uint32_t v)
-{
-    uint8_t *q = wr_ptr(k, off);
-    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+    if (off + 4 <= k.win) {
+        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+        k.dirty = true;
+    } else if (off >= k.win) {
+        uint8_t *q = k.p + off;
+        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+    } else {
+        wr16(k, off, v);
+        wr16(k, off + 2, v >> 16);
+    }
 }
 
-// Bounds check of the BPF code ("data + n > data_end").  `lim` is the smaller of the frame length
-// and the bytes present (the staged window, the host path's DMA window); running past it inside
-// the frame marks the frame `cut`: it is finished from HBM, or handed back to the host path.
-template <class F>
-__device__ __forceinline__ bool beyond(F &k, int end)
+// Bounds check of the BPF code ("data + n > data_end").  With a header window smaller than the
+// frame, running past the window marks the frame `cut` (the host path re-runs it whole).
+__device__ __forceinline__ bool beyond(BrFrame &k, int end)
 {
     if (end <= k.lim) return false;
     if (end <= k.len) k.cut = true;
     return true;
 }
 
-template <bool STATS, class F>
-__device__ __forceinline__ uint32_t record(F &k, uint32_t verdict)   // record_verdict, xdp.c:54-70
+template <bool STATS>
+__device__ __forceinline__ uint32_t record(BrFrame &k, uint32_t verdict)   // record_verdict, xdp.c:54-70
 {
     uint32_t idx = (verdict >> 3) & 0x0fu;
     k.last_verdict = verdict;
@@ -180,8 +179,7 @@ __device__ __forceinline__ uint32_t record(F &k, uint32_t verdict)   // record_v
 }
 
 // ---- parser.h ----------------------------------------------------------------------------
-template <class F>
-__device__ __forceinline__ int parse_underlay(F &k)
+__device__ __forceinline__ int parse_underlay(BrFrame &k)
 {
     k.verdict = V_NOT_SCION;
     int off = 14;
@@ -230,8 +228,7 @@ __device__ __forceinline__ int parse_underlay(F &k)
     return off;
 }
 
-template <class F>
-__device__ __forceinline__ int parse_scion_path(F &k, int off)
+__device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
 {
     k.verdict = V_PARSE_ERROR;
     k.meta = off;
@@ -261,8 +258,7 @@ __device__ __forceinline__ int parse_scion_path(F &k, int off)
     return off;
 }
 
-template <class F>
-__device__ __forceinline__ int parse_scion(F &k, int off)
+__device__ __forceinline__ int parse_scion(BrFrame &k, int off)
 {
     k.verdict = V_PARSE_ERROR;
     int sc = off;
@@ -282,11 +278,9 @@ __device__ __forceinline__ int parse_scion(F &k, int off)
 }
 
 // ---- path_processing.h ---------------------------------------------------------------------
-template <class F>
-__device__ __forceinline__ uint32_t cons_at(const F &k, int inf) { return rd8(k, inf) & 1u; }
+__device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return rd8(k, inf) & 1u; }
 
-template <class F>
-__device__ __forceinline__ void defer_verify(F &k, int inf, int hf, uint32_t beta_nbo)
+__device__ __forceinline__ void defer_verify(BrFrame &k, int inf, int hf, uint32_t beta_nbo)
 {
     k.need_mac = true;
     k.mi[0] = (beta_nbo & 0xffffu) << 16;
@@ -297,8 +291,7 @@ __device__ __forceinline__ void defer_verify(F &k, int inf, int hf, uint32_t bet
     k.mac_hi = rd16(k, hf + 10);
 }
 
-template <class F>
-__device__ __forceinline__ bool as_ingress(F &k)
+__device__ __forceinline__ bool as_ingress(BrFrame &k)
 {
     if (rd8(k, k.hf) & 0x03u) {
         k.verdict = V_ROUTER_ALERT;
@@ -330,8 +323,7 @@ __device__ __forceinline__ bool as_ingress(F &k)
     return true;
 }
 
-template <class F>
-__device__ __forceinline__ bool as_egress(F &k, uint32_t as_ing_ifid)
+__device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
 {
     k.verdict = A_ABORTED;
     if (rd8(k, k.hf) & 0x03u) {
@@ -364,8 +356,7 @@ __device__ __forceinline__ int int_iface(uint32_t ifindex)
     return -1;
 }
 
-template <class F>
-__device__ __forceinline__ int ingress_lookup(const F &k)
+__device__ __forceinline__ int ingress_lookup(const BrFrame &k)
 {
     for (uint32_t i = 0; i < s_br.n_ing; ++i) {
         const DevBrIngress &e = s_br.ingress[i];
@@ -402,8 +393,7 @@ __device__ __forceinline__ int route_lookup(uint32_t family, uint32_t d0, uint32
 }
 
 // bpf_fib_lookup return-code handling shared by the fib_lookup_* helpers; false = stop
-template <class F>
-__device__ __forceinline__ bool fib_result(F &k, int r)
+__device__ __forceinline__ bool fib_result(BrFrame &k, int r)
 {
     int ret = r >= 0 ? s_br.routes[r].ret : 4;   // no route: BPF_FIB_LKUP_RET_NOT_FWDED
     if (ret >= 1 && ret <= 3) {
@@ -427,16 +417,14 @@ __device__ __forceinline__ bool fib_result(F &k, int r)
 // The family-dependent field updates below are written as selects, not branches: LLVM would
 // otherwise sink the v4 and v6 stores into one store through a pointer phi and keep the
 // frame's address fields in scratch.
-template <class F>
-__device__ __forceinline__ void set_dst(F &k, const uint32_t a[4])
+__device__ __forceinline__ void set_dst(BrFrame &k, const uint32_t a[4])
 {
     const bool v4 = k.family == HFV_AF_INET;
     k.v4_dst = v4 ? a[0] : k.v4_dst;
 #pragma unroll
     for (int i = 0; i < 4; ++i) k.v6_dst[i] = v4 ? k.v6_dst[i] : a[i];
 }
-template <class F>
-__device__ __forceinline__ void set_src(F &k, const uint32_t a[4])
+__device__ __forceinline__ void set_src(BrFrame &k, const uint32_t a[4])
 {
     const bool v4 = k.family == HFV_AF_INET;
     k.v4_src = v4 ? a[0] : k.v4_src;
@@ -446,8 +434,7 @@ __device__ __forceinline__ void set_src(F &k, const uint32_t a[4])
     k.v6_hop = v4 ? k.v6_hop : 64u;
 }
 
-template <class F>
-__device__ __forceinline__ int fib_as_egress(F &k, const DevBrEgress &link)
+__device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link)
 {
     k.udp_dst = link.remote_port;
     k.udp_src = link.local_port;
@@ -458,8 +445,7 @@ __device__ __forceinline__ int fib_as_egress(F &k, const DevBrEgress &link)
     return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
 }
 
-template <class F>
-__device__ __forceinline__ int fib_egress_br(F &k, const DevBrEgress &sib)
+__device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
 {
     k.udp_dst = sib.remote_port;
     set_dst(k, sib.remote);
@@ -481,8 +467,7 @@ __device__ __forceinline__ int fib_egress_br(F &k, const DevBrEgress &sib)
     return (int)out_if;
 }
 
-template <class F>
-__device__ __forceinline__ int fib_ip_forward(F &k)
+__device__ __forceinline__ int fib_ip_forward(BrFrame &k)
 {
     int r;
     if (k.family == HFV_AF_INET)   // hdr->ip.v4->daddr
@@ -504,8 +489,7 @@ __device__ __forceinline__ uint32_t fold_checksum(uint64_t c)
     return (uint32_t)(c & 0xffffu);
 }
 
-template <class F>
-__device__ __forceinline__ void rewrite(F &k)
+__device__ __forceinline__ void rewrite(BrFrame &k)
 {
     wr32(k, 0, k.dmac_lo); wr16(k, 4, k.dmac_hi);
     wr32(k, 6, k.smac_lo); wr16(k, 10, k.smac_hi);
@@ -557,8 +541,8 @@ __device__ __forceinline__ void rewrite(F &k)
 // ---- xdp.c: process_packet -----------------------------------------------------------------
 // Returns the action (> 0 ends the frame), 0 (fall through to the MAC check without a record:
 // the bare `return 0`/ABORT paths) or -1 (rewritten, go to the MAC check).
-template <bool STATS, class F>
-__device__ __forceinline__ int process_packet(F &k)
+template <bool STATS>
+__device__ __forceinline__ int process_packet(BrFrame &k)
 {
     k.egress_ifindex = -1;
     int off = parse_underlay(k);
@@ -611,21 +595,17 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 }
 
 // ---- kernel ------------------------------------------------------------------------------------
-// The frame's border_router() (xdp.c:250-283).  Returns false for an LDS-mode frame that was
-// cut at the staged window: nothing of it was written or counted, the caller runs it from HBM.
-template <bool STATS, class F>
-__device__ __forceinline__ bool br_frame(F &k, uint64_t i, const DevKeyTable *keys, const Lane &l,
+template <bool STATS>
+__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTable *keys, const Lane &l,
                                          uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
                                          int32_t *__restrict__ egress)
 {
     int a = process_packet<STATS>(k);
-    if (k.cut) {
-        if constexpr (F::kLds) return false;
-        // headers reach past the bytes the host path moved: untouched, uncounted, re-run whole
+    if (k.cut) {   // headers reach past the window: untouched, uncounted, caller re-runs it whole
         action[i] = HFV_BR_ACTION_RETRY;
         verdict[i] = 0;
         egress[i] = -1;
-        return true;
+        return;
     }
     if (a <= 0) {
         // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
@@ -645,23 +625,6 @@ __device__ __forceinline__ bool br_frame(F &k, uint64_t i, const DevKeyTable *ke
     action[i] = (uint8_t)a;
     verdict[i] = (uint8_t)k.last_verdict;
     egress[i] = k.egress_ifindex;
-    return true;
-}
-
-// The rare rerun of a frame cut at the staged window, kept out of line so that its register
-// needs do not weigh on the staged parser.
-template <bool STATS>
-__device__ __attribute__((noinline)) void br_frame_hbm(uint8_t *p, int len, int lim, uint32_t ifx, uint64_t i,
-                                                      const DevKeyTable *keys, uint8_t *action, uint8_t *verdict,
-                                                      int32_t *egress)
-{
-    BrFrameT<false> k = {};
-    k.p = p;
-    k.len = len;
-    k.lim = lim;
-    k.ifindex = ifx;
-    const Lane l = lane_bases();
-    br_frame<STATS>(k, i, keys, l, action, verdict, egress);
 }
 
 // One wave = one tile of 64 consecutive frames (lane = frame).  WIN > 0: the tile's first WIN
@@ -697,7 +660,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
     // The tile's header rows and the lane's own length / ingress ifindex are fetched one tile
     // ahead, all before anything of the current tile is loaded: vmcnt retires in issue order,
-    // so a load issued after the prefetch would make its wait cover the prefetch too.
+    // so a load of the current tile issued after the prefetch would wait for the prefetch too.
     uint4 pre[C];
     uint32_t pre_len = 0, pre_ifx = 0;
     auto fetch = [&](uint64_t tt) {
@@ -730,31 +693,19 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         const uint32_t len = pre_len, ifx = pre_ifx;
         if (t + nwaves < ntiles) fetch(t + nwaves);
         uint64_t i = t * 64 + lane;
-        bool dirty = false, defer = false;
-        const int flen = (int)(len <= maxlen ? len : maxlen);
-        const int flim = flen < (int)window ? flen : (int)window;
+        bool dirty = false;
         if (i < n) {
-            if constexpr (WIN > 0) {
-                BrFrameT<true> k = {};
-                k.p = pkts + i * slot;
-                k.row = (wib * 64 + lane) * kBrRow;
-                k.len = flen;
-                k.lim = flim < WIN ? flim : WIN;
-                k.ifindex = ifx;
-                defer = !br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
-                dirty = k.dirty;
-            } else {
-                BrFrameT<false> k = {};
-                k.p = pkts + i * slot;
-                k.len = flen;
-                k.lim = flim;
-                k.ifindex = ifx;
-                br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
-            }
+            BrFrame k = {};
+            k.p = pkts + i * slot;
+            k.win = WIN;
+            k.row = (wib * 64 + lane) * kBrRow;
+            k.len = (int)(len <= maxlen ? len : maxlen);
+            k.lim = k.len < (int)window ? k.len : (int)window;
+            k.ifindex = ifx;
+            br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
+            dirty = k.dirty;
         }
         if constexpr (WIN > 0) {
-            if (defer)   // rare: headers past the staged window, again straight from HBM
-                br_frame_hbm<STATS>(pkts + i * slot, flen, flim, ifx, i, &st->keys, action, verdict, egress);
             // write the rewritten rows back: 16-byte stores, WIN / 16 lanes per frame
             uint64_t dmask = __ballot(dirty);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -136,8 +136,10 @@ int hfv_cmac_tags(hfv_ctx *ctx, const struct macinput *mi, const uint8_t *key_in
 int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                              void *stream, float *kernel_ms);
 /* Host-memory batch (config 5 path): records and bitmap in HOST memory; returns when
- * pass_bits is complete.  Pageable records are staged through pinned buffers with H2D /
- * kernel / D2H overlapped over chunks; records inside a buffer registered with
+ * pass_bits is complete.  From pageable records, host threads (HFV_HOST_THREADS, default
+ * min(8, cores)) gather each record's InfoField and HopField (the 20 bytes the verifier
+ * reads) into 24-byte pinned staging records, chunk by chunk, with gather / H2D / kernel /
+ * D2H overlapped over chunks on two streams; records inside a buffer registered with
  * hfv_host_register (an RX ring) are read by the kernel in place over PCIe (zero-copy),
  * and a registered pass_bits is written in place. */
 int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits);

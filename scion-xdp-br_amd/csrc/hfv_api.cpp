@@ -13,6 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -168,6 +171,7 @@ struct hfv_ctx {
     uint8_t *brh_dwin[2] = {nullptr, nullptr};
     uint8_t *brh_dio[2] = {nullptr, nullptr};   // len u16 | ifindex u32 | action u8 | verdict u8 | egress i32
     uint8_t *brh_hio[2] = {nullptr, nullptr};   // pinned twin of brh_dio
+    uint8_t *brh_hwin[2] = {nullptr, nullptr};  // pinned twin of brh_dwin (packed header windows)
     uint64_t *brh_dstats = nullptr;
     // host buffers registered with hfv_host_register (mapped: the kernels can address them)
     struct HostRange {
@@ -345,6 +349,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
     }
     for (int i = 0; i < 2; ++i) {
         if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
+        if (ctx->brh_hwin[i]) (void)hipHostFree(ctx->brh_hwin[i]);
         if (ctx->brh_dio[i]) (void)hipFree(ctx->brh_dio[i]);
         if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
     }
@@ -448,13 +453,6 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
         if (!rc) rc = keymap_open_ro(path, &m);
     }
     if (rc) return fail(rc, "cannot attach key map %s", path);
-    for (int i = 0; i < 2; ++i) {
-        if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
-        if (ctx->brh_dio[i]) (void)hipFree(ctx->brh_dio[i]);
-        if (ctx->brh_hio[i]) (void)hipHostFree(ctx->brh_hio[i]);
-    }
-    if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
-    if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
     keymap_close(ctx->keymap);
     ctx->keymap = m;
     strcpy(ctx->keymap_path, path);
@@ -732,6 +730,133 @@ int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_
 // the windows + metadata, the kernel (stride = window, lengths clamped to the caller's slot),
 // strided D2H of the rewritten windows + results.  Then frames marked HFV_BR_ACTION_RETRY
 // (headers beyond the window) go through again with whole slots.
+}  // extern "C"
+
+// Compact staging record of the host path: INF (8 B) at 0, HF (12 B) at 8, 4 B pad.
+static constexpr size_t kHostRec = 24;
+
+// Host threads for staging copies: HFV_HOST_THREADS, default min(8, cores).
+static int host_threads()
+{
+    static const int t = [] {
+        const char *e = getenv("HFV_HOST_THREADS");
+        int v = e ? atoi(e) : 0;
+        if (v <= 0) {
+            unsigned hc = std::thread::hardware_concurrency();
+            v = hc ? (int)(hc < 8 ? hc : 8) : 4;
+        }
+        return v;
+    }();
+    return t;
+}
+
+// Persistent host worker threads for the staging copies (spawning threads per copy cost more
+// than the copies: 32 spawns per 2^20-frame router batch).  Part 0 of every job runs on the
+// calling thread, parts 1..nt-1 on the workers.  Jobs come from one ctx thread at a time.
+class HostPool {
+  public:
+    explicit HostPool(int nt) : nt_(nt)
+    {
+        for (int k = 1; k < nt_; ++k) th_.emplace_back([this, k] { work(k); });
+    }
+    ~HostPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void run(size_t n, const std::function<void(size_t, size_t)> &fn)
+    {
+        std::unique_lock<std::mutex> lk(job_m_);   // one job at a time
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            n_ = n;
+            left_ = nt_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0, n / nt_);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        fn_ = nullptr;
+    }
+    int threads() const { return nt_; }
+
+  private:
+    void work(int k)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t, size_t)> *fn;
+            size_t n;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+                n = n_;
+            }
+            (*fn)(n * k / nt_, n * (k + 1) / nt_);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    int nt_;
+    std::vector<std::thread> th_;
+    std::mutex m_, job_m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t, size_t)> *fn_ = nullptr;
+    size_t n_ = 0;
+    int left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+static HostPool &host_pool()
+{
+    static HostPool pool(host_threads());
+    return pool;
+}
+
+// fn(a, b) over [0, n) split into host_threads() contiguous parts (inline below 8192 items).
+template <class F>
+static void parallel_rows(size_t n, F fn)
+{
+    if (host_threads() <= 1 || n < 8192) {
+        fn((size_t)0, n);
+        return;
+    }
+    host_pool().run(n, std::function<void(size_t, size_t)>(fn));
+}
+
+// dst[i] = {INF, HF} of src record i (the verifier's 20 bytes).
+static void gather_hf(uint8_t *dst, const uint8_t *src, size_t stride, uint32_t inf_off, uint32_t hf_off, size_t n)
+{
+    parallel_rows(n, [=](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            const uint8_t *r = src + i * stride;
+            uint8_t *d = dst + i * kHostRec;
+            memcpy(d, r + inf_off, 8);
+            memcpy(d + 8, r + hf_off, 12);
+        }
+    });
+}
+
+// Row copies between frames in their slots and packed windows: dst row i <- src row i.
+static void copy_rows(uint8_t *dst, size_t dpitch, const uint8_t *src, size_t spitch, size_t width, size_t n)
+{
+    parallel_rows(n, [=](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) memcpy(dst + i * dpitch, src + i * spitch, width);
+    });
+}
+
+extern "C" {
+
 static const size_t kBrChunk = (size_t)1 << 16;
 
 static int brh_buffers(hfv_ctx *ctx, size_t window)
@@ -748,8 +873,10 @@ static int brh_buffers(hfv_ctx *ctx, size_t window)
         for (int i = 0; i < 2; ++i) {
             HIP_TRY(hipStreamSynchronize(ctx->hstream[i]));
             if (ctx->brh_dwin[i]) (void)hipFree(ctx->brh_dwin[i]);
-            ctx->brh_dwin[i] = nullptr;
+            if (ctx->brh_hwin[i]) (void)hipHostFree(ctx->brh_hwin[i]);
+            ctx->brh_dwin[i] = ctx->brh_hwin[i] = nullptr;
             HIP_TRY(hipMalloc((void **)&ctx->brh_dwin[i], kBrChunk * window));
+            HIP_TRY(hipHostMalloc((void **)&ctx->brh_hwin[i], kBrChunk * window, hipHostMallocDefault));
         }
         ctx->brh_win_cap = window;
     }
@@ -765,7 +892,9 @@ static int brh_chunk(hfv_ctx *ctx, int sl, uint8_t *frames, size_t fstride, size
     memcpy(hio, len, cnt * 2);
     memcpy(hio + kBrChunk * 2, ifx, cnt * 4);
     HIP_TRY(hipMemcpyAsync(dio, hio, kBrChunk * 6, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpy2DAsync(ctx->brh_dwin[sl], window, frames, fstride, window, cnt, hipMemcpyHostToDevice, st));
+    // the header windows, packed by host threads into pinned staging, then one linear DMA
+    copy_rows(ctx->brh_hwin[sl], window, frames, fstride, window, cnt);
+    HIP_TRY(hipMemcpyAsync(ctx->brh_dwin[sl], ctx->brh_hwin[sl], cnt * window, hipMemcpyHostToDevice, st));
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
@@ -775,13 +904,17 @@ static int brh_chunk(hfv_ctx *ctx, int sl, uint8_t *frames, size_t fstride, size
                               ctx->brh_dstats, st);
     rc = after_launch(ctx, st, e, "br_process launch");
     if (rc) return rc;
-    HIP_TRY(hipMemcpy2DAsync(frames, fstride, ctx->brh_dwin[sl], window, window, cnt, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ctx->brh_hwin[sl], ctx->brh_dwin[sl], cnt * window, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(hio + kBrChunk * 6, dio + kBrChunk * 6, kBrChunk * 6, hipMemcpyDeviceToHost, st));
     return 0;
 }
 
-static void brh_results(hfv_ctx *ctx, int sl, size_t cnt, uint8_t *action, uint8_t *verdict, int32_t *egress)
+// A retired chunk (its stream synchronized): the rewritten windows back into the frames
+// (host threads), and the per-frame results.
+static void brh_results(hfv_ctx *ctx, int sl, uint8_t *frames, size_t fstride, size_t window, size_t cnt,
+                        uint8_t *action, uint8_t *verdict, int32_t *egress)
 {
+    copy_rows(frames, fstride, ctx->brh_hwin[sl], window, window, cnt);
     const uint8_t *hio = ctx->brh_hio[sl];
     memcpy(action, hio + kBrChunk * 6, cnt);
     memcpy(verdict, hio + kBrChunk * 7, cnt);
@@ -871,7 +1004,8 @@ int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16
         if (c >= 2) {
             HIP_TRY(hipStreamSynchronize(ctx->hstream[sl]));
             size_t f = first_of[sl];
-            brh_results(ctx, sl, cnt_of[sl], action + f, verdict + f, egress_ifindex + f);
+            brh_results(ctx, sl, frames + f * slot, slot, window, cnt_of[sl], action + f, verdict + f,
+                        egress_ifindex + f);
         }
         if (c >= nchunks) continue;
         size_t first = c * kBrChunk, cnt = n - first < kBrChunk ? n - first : kBrChunk;
@@ -907,7 +1041,7 @@ int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16
             if (rc == 0 && hipStreamSynchronize(ctx->hstream[0]) != hipSuccess) rc = fail(-EIO, "retry chunk");
             for (size_t k = 0; rc == 0 && k < cnt; ++k) {
                 size_t j = idx[k];
-                memcpy(frames + j * slot, bounce + k * slot, slot);
+                memcpy(frames + j * slot, ctx->brh_hwin[0] + k * slot, slot);
                 action[j] = ctx->brh_hio[0][kBrChunk * 6 + k];
                 verdict[j] = ctx->brh_hio[0][kBrChunk * 7 + k];
                 memcpy(&egress_ifindex[j], ctx->brh_hio[0] + kBrChunk * 8 + 4 * k, 4);
@@ -986,51 +1120,6 @@ static int verify_records_zero_copy(hfv_ctx *ctx, const uint8_t *drecs, size_t s
     return 0;
 }
 
-}  // extern "C"
-
-// Compact staging record of the host path: INF (8 B) at 0, HF (12 B) at 8, 4 B pad.
-static constexpr size_t kHostRec = 24;
-
-// Host threads for the staging gather: HFV_HOST_THREADS, default min(8, cores).
-static int host_threads()
-{
-    static const int t = [] {
-        const char *e = getenv("HFV_HOST_THREADS");
-        int v = e ? atoi(e) : 0;
-        if (v <= 0) {
-            unsigned hc = std::thread::hardware_concurrency();
-            v = hc ? (int)(hc < 8 ? hc : 8) : 4;
-        }
-        return v;
-    }();
-    return t;
-}
-
-// dst[i] = {INF, HF} of src record i (the verifier's 20 bytes), split over nthreads threads.
-static void gather_hf(uint8_t *dst, const uint8_t *src, size_t stride, uint32_t inf_off, uint32_t hf_off, size_t n,
-                      int nthreads)
-{
-    auto part = [=](size_t a, size_t b) {
-        for (size_t i = a; i < b; ++i) {
-            const uint8_t *r = src + i * stride;
-            uint8_t *d = dst + i * kHostRec;
-            memcpy(d, r + inf_off, 8);
-            memcpy(d + 8, r + hf_off, 12);
-        }
-    };
-    if (nthreads <= 1 || n < 8192) {
-        part(0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(nthreads - 1);
-    for (int k = 1; k < nthreads; ++k) th.emplace_back(part, n * k / nthreads, n * (k + 1) / nthreads);
-    part(0, n / nthreads);
-    for (auto &t : th) t.join();
-}
-
-extern "C" {
-
 // Host batch: chunks of records go host -> pinned -> device, verified, bitmap back; two
 // streams alternate so chunk k's copy-in overlaps chunk k-1's kernel and copy-out.  Records
 // in a registered buffer (hfv_host_register) take the zero-copy path instead.
@@ -1067,7 +1156,6 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         }
         ctx->host_chunk = chunk * kHostRec;
     }
-    const int nthreads = host_threads();
     size_t nchunks = (n + chunk - 1) / chunk;
     size_t pending_words[2] = {0, 0};
     size_t pending_first[2] = {0, 0};
@@ -1080,8 +1168,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         }
         if (c >= nchunks) continue;
         size_t first = c * chunk, cnt = n - first < chunk ? n - first : chunk;
-        gather_hf(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, stride, ctx->inf_off, ctx->hf_off, cnt,
-                  nthreads);
+        gather_hf(ctx->h_pin[slot], (const uint8_t *)recs + first * stride, stride, ctx->inf_off, ctx->hf_off, cnt);
         HIP_TRY(hipMemcpyAsync(ctx->d_rec[slot], ctx->h_pin[slot], cnt * kHostRec, hipMemcpyHostToDevice, st));
         DevState *ds;
         int rc = publish_keys(ctx, st, &ds);

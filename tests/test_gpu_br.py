@@ -170,3 +170,27 @@ def test_fuzz_parity_unstaged_slot(gpu_ctx):
     hops = F.hop_inputs(brs, True, MAC)
     frames, lens, ifidx = F.fuzz_batch(hops, "br1", True, 6000, seed=9, slot=1032, payload_max=1000)
     _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", True), T.KEYS[1])
+
+
+def test_host_path_survives_keymap_attach(gpu_ctx, tmp_path, monkeypatch):
+    """Attaching the pinned key map after the host path ran must leave the host path's
+    staging buffers alone (regression: the attach once freed them without forgetting them,
+    so the next host batch or ctx destruction used freed memory)."""
+    monkeypatch.setenv("HFV_PIN_DIR", str(tmp_path))
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 2000, seed=17, slot=512)
+    ref = frames.copy()
+    oa, ov, oe, _ = orc.br_process(ref, lens, ifidx, T.br_config("br1"), orc.hop_key(T.KEYS[1]))
+    gpu_ctx.br_set_config(T.br_config("br1"))
+    gpu_ctx.key_add(0, T.KEYS[1])
+    for attach in (False, True):
+        got = frames.copy()
+        a = np.zeros(2000, np.uint8)
+        v = np.zeros(2000, np.uint8)
+        e = np.zeros(2000, np.int32)
+        gpu_ctx.br_process_host(got, 512, lens, ifidx, 2000, a, v, e, None, window=128)
+        assert (a == oa).all() and (v == ov).all() and (e == oe).all() and (got == ref).all()
+        if not attach:
+            gpu_ctx.attach_keymap(hfv.keymap_path("br1"))   # an empty map: re-add the key through it
+            gpu_ctx.key_add(0, T.KEYS[1])

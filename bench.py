@@ -152,8 +152,12 @@ def lds_bound_at_clock(keysel, mhz):
     if not mhz or keysel != "zero":
         return {}
     cus = torch.cuda.get_device_properties(0).multi_processor_count
+    # VALU: per 64-packet tile 145 v_perm_b32 (4 SIMD cycles per wave64 instruction, measured
+    # half rate) + 132 full-rate instructions (2 cycles); 4 SIMDs per CU
+    valu_cycles_per_pkt = (145 * 4 + 132 * 2) / 64.0
     return {"service_shader_mhz": round(mhz, 1),
-            "lds_bound_mpkts_at_service_clock": round(cus * 32 * mhz * 1e6 / 146.2 / 1e6, 1)}
+            "lds_bound_mpkts_at_service_clock": round(cus * 32 * mhz * 1e6 / 146.2 / 1e6, 1),
+            "valu_bound_mpkts_at_service_clock": round(cus * 4 * mhz * 1e6 / valu_cycles_per_pkt / 1e6, 1)}
 
 
 def pmc_traffic(keysel, n, service=False):

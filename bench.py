@@ -437,7 +437,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default 200 (hf), 10 (br), 5 (br-host)")
     ap.add_argument("--warmup", type=int, default=None, help="default 20 (hf), 3 (br), 1 (br-host)")
-    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU (config 2: 2^20)")
+    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU (config 2: 2^20); with --strong, in total")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --n records in total, sliced over the ranks on 64-record boundaries")
     ap.add_argument("--keysel", choices=["zero", "ifid"], default="zero")
     ap.add_argument("--big-n", type=int, default=1 << 24, help="HBM-resident run size (0 = skip)")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
@@ -466,12 +468,16 @@ def main():
     if args.workload == "br-host":
         return run_br_host(args, rank, world, local)
     keysel = hfv.KEYSEL_IFID if args.keysel == "ifid" else hfv.KEYSEL_ZERO
-    n = args.n
+    if args.strong:   # a fixed total, sliced over the ranks (scion_hfv.shard_range)
+        first, last = hfv.shard_range(args.n, world, rank)
+        n, total = last - first, args.n
+    else:             # weak: every rank verifies its own n records
+        n, first, total = args.n, rank * args.n, world * args.n
 
     ctx = make_ctx(local, keysel)
     stream = torch.cuda.current_stream().cuda_stream   # int handle (0 = default stream)
     recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
-    ctx.gen_records(recs, n, SEED_RECORDS, first_index=rank * n, stream=stream)
+    ctx.gen_records(recs, n, SEED_RECORDS, first_index=first, stream=stream)
     bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
 
     # --- launch path (hfv_verify_records: one launch + table fill per batch) ---------------
@@ -479,7 +485,7 @@ def main():
         ctx.verify_records(recs, n, bits, stream=stream)
     torch.cuda.synchronize()
     # the verdicts must be right before anything is timed
-    assert popcount(bits) == expected_pass_count(n, rank * n), "verify bitmap disagrees with generator truth"
+    assert popcount(bits) == expected_pass_count(n, first), "verify bitmap disagrees with generator truth"
     launch_elapsed = timed_steps(world, args.steps, lambda: ctx.verify_records(recs, n, bits, stream=stream))
     k_mean, k_med = kernel_ms(ctx, recs, n, bits, stream, max(20, min(args.steps, 200)))
 
@@ -491,7 +497,7 @@ def main():
     for _ in range(args.warmup):
         ctx.service_submit(recs, n, bits)
     ctx.service_stop()
-    assert popcount(bits) == expected_pass_count(n, rank * n), "service bitmap disagrees with generator truth"
+    assert popcount(bits) == expected_pass_count(n, first), "service bitmap disagrees with generator truth"
     svc = {}
 
     def service_run():
@@ -502,7 +508,7 @@ def main():
         svc["shader_mhz"] = ctx.service_shader_mhz()
 
     svc_elapsed = timed_steps(world, 1, service_run)
-    assert popcount(bits) == expected_pass_count(n, rank * n)
+    assert popcount(bits) == expected_pass_count(n, first)
     headline = args.mode
     elapsed = svc_elapsed if headline == "service" else launch_elapsed
 
@@ -518,12 +524,12 @@ def main():
         achieved = bytes_per_launch / (k_mean * 1e-3) / 1e9
         kern = {"kernel": "k_verify_records", "kernel_ms_mean": round(k_mean, 5),
                 "kernel_ms_median": round(k_med, 5), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
-    per_launch = {"mpkts": round(world * n * args.steps / launch_elapsed / 1e6, 2),
+    per_launch = {"mpkts": round(total * args.steps / launch_elapsed / 1e6, 2),
                   "ms_per_step": round(launch_elapsed / args.steps * 1e3, 5),
                   "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(k_med, 5),
                   "kernel_mpkts": round(n / k_mean / 1e3, 1),
                   "frac": round(bytes_per_launch / (k_mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    service = {"mpkts": round(world * n * args.steps / svc_elapsed / 1e6, 2),
+    service = {"mpkts": round(total * args.steps / svc_elapsed / 1e6, 2),
                "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4),
                "shader_mhz": round(svc["shader_mhz"], 1) if svc["shader_mhz"] else None}
 
@@ -531,18 +537,19 @@ def main():
 
     result = {
         "metric": "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets",
-        "value": round(world * n * args.steps / elapsed / 1e6, 2),
+        "value": round(total * args.steps / elapsed / 1e6, 2),
         "unit": "Mpkt/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (64 B SCION records, splitmix64 seed 0x5C100001, 1/16 corrupted MACs; generated on device)",
-        "config": {"workload": f"config {'3' if keysel else '2'}: {n} x 64 B records per GPU, "
+        "config": {"workload": f"config {'3' if keysel else '2'}: "
+                               f"{f'{total} x 64 B records in total' if args.strong else f'{n} x 64 B records per GPU'}, "
                                f"{'256 ingress-interface keys (KEYSEL_IFID)' if keysel else 'single AS key'}",
                    "records_per_gpu": n, "record_bytes": 64, "keysel": args.keysel,
                    "parallelism": f"batch-sharded x{world}, no collective"},

@@ -266,8 +266,10 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
                    size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats,
                    void *stream);
 /* Config 5: frames in HOST memory (an RX ring of `slot`-byte slots).  Chunk by chunk, only
- * the first `window` bytes of each slot cross PCIe (strided DMA straight from `frames`;
- * register the ring once with hfv_host_register so no bounce copy is needed), are processed
+ * the first `window` bytes of each slot cross PCIe (host threads pack them into pinned
+ * staging for one linear DMA each way and write the rewritten windows back; a ring
+ * registered with hfv_host_register is instead read and written in place by the kernel over
+ * PCIe), are processed
  * exactly as hfv_br_process does, and the rewritten window is copied back in place.  Frames
  * whose headers reach past the window are run again with the whole slot, so the result is
  * identical to hfv_br_process on the full frames.  len, ingress_ifindex, action, verdict,

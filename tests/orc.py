@@ -12,7 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "libhfvoracle.so")
+# HFV_ORACLE_SO: another build of the same checker (the sanitizer build, tests/test_sanitize.py)
+ORACLE_SO = os.environ.get("HFV_ORACLE_SO") or os.path.join(ORACLE_DIR, "libhfvoracle.so")
 REF_SO = os.path.join(ORACLE_DIR, "_ref", "libaesref.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 

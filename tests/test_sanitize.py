@@ -1,6 +1,7 @@
-"""The CPU checker's C code under AddressSanitizer + UBSan: builds
-oracle/_san/libhfvoracle_san.so and runs tests/san_driver.py against it in a child process
-with libasan preloaded.  CPU only."""
+"""Host code under AddressSanitizer + UBSan: the CPU checker's C code
+(oracle/_san/libhfvoracle_san.so driven by tests/san_driver.py in a child process with libasan
+preloaded) and the product's host-side C++ (aes.h API, pinned key and counter maps) linked
+into tests/host_san_driver.cpp.  CPU only."""
 import os
 import subprocess
 import sys
@@ -34,3 +35,22 @@ def test_oracle_under_asan_ubsan():
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert "san ok" in r.stdout
+
+
+def test_product_host_code_under_asan_ubsan(tmp_path):
+    csrc = os.path.join(ROOT, "scion-xdp-br_amd", "csrc")
+    exe = str(tmp_path / "host_san")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", "-I" + os.path.join(ROOT, "include"), "-I" + csrc, "-o", exe,
+           os.path.join(ROOT, "tests", "host_san_driver.cpp")] + [
+               os.path.join(csrc, f) for f in ("hfv_aes_host.cpp", "hfv_keymap.cpp", "hfv_statsmap.cpp")]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    if b.returncode != 0 and "sanitize" in b.stderr:
+        pytest.skip("sanitizer runtime unavailable: " + b.stderr[-300:])
+    assert b.returncode == 0, b.stderr[-3000:]
+    pin = tmp_path / "pin"
+    pin.mkdir()
+    env = dict(os.environ, HFV_PIN_DIR=str(pin), ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "host san ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -230,7 +230,7 @@ def test_full_size_properties(ctx, n):
 
 def test_host_path_matches_device(ctx):
     ctx.key_add(0, orc.KEY_1111)
-    n = (1 << 21) + 777   # crosses the 1 Mi-record chunk boundary twice
+    n = (1 << 21) + 777   # 8 full 2^18-record staging chunks and a ragged ninth
     recs = torch.empty((n, 64), dtype=torch.uint8, device=DEV)
     ctx.gen_records(recs, n, orc.SEED_RECORDS)
     dbits = new_bits(n)
@@ -239,6 +239,15 @@ def test_host_path_matches_device(ctx):
     hbits = np.zeros((n + 63) // 64, dtype=np.uint64)
     ctx.verify_records_host(hrecs, n, hbits)
     assert np.array_equal(hbits, bits_np(dbits, n))
+    # a wider stride: the host threads gather INF/HF from 128-byte slots
+    m = 300001
+    wide = np.zeros((m, 128), dtype=np.uint8)
+    wide[:, :64] = hrecs[:m]
+    wbits = np.zeros((m + 63) // 64, dtype=np.uint64)
+    ctx.verify_records_host(wide, m, wbits, stride=128)
+    want = bits_np(dbits, n)[: (m + 63) // 64].copy()
+    want[-1] &= np.uint64((1 << (m % 64)) - 1) if m % 64 else np.uint64(~0)
+    assert np.array_equal(wbits, want)
 
 
 def test_host_zero_copy_ring(ctx):

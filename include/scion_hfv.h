@@ -149,7 +149,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
  * (border_router, xdp.c:250-284, runs for every packet without a per-packet load): one
  * persistent grid per ctx keeps the AES tables (and, for KEYSEL_IFID, the key image)
  * resident in LDS and verifies batches as the host posts them, with the same verdict
- * semantics as hfv_verify_records.  Batches are posted into a 64-entry descriptor ring in
+ * semantics as hfv_verify_records.  Batches are posted into a 256-entry descriptor ring in
  * pinned host memory; no kernel launch or table fill per batch, and a batch's tail
  * overlaps the next batch's start.
  *   - Key-table, keysel or record-layout changes take effect at the next submit (the
@@ -163,7 +163,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
 /* Launch the service grid (no-op if running).  idle_ms 0: 1000 ms. */
 int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms);
 /* Post one batch (device pointers, as hfv_verify_records; starts the service if needed).
- * Returns its ticket (1, 2, ...) in *ticket.  Blocks only while 64 batches are in flight.
+ * Returns its ticket (1, 2, ...) in *ticket.  Blocks only while 256 batches are in flight.
  * Host-ordered, not stream-ordered: the records must be in place and the bitmap must no
  * longer be written by other work when the call is made (synchronize their producers). */
 int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,

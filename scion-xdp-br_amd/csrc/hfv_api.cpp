@@ -193,6 +193,7 @@ struct hfv_ctx {
     SvcDesc *svc_mirror = nullptr;   // device copy of the descriptor ring (the grid's relay writes it)
     unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
     uint64_t svc_next = 1;           // next ticket
+    uint64_t svc_tag = 0;            // generation of the running grid << 40 (see s_svc_tag)
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
 };
 
@@ -1188,7 +1189,9 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
 
 // ---- resident verify service ----------------------------------------------------------
 // The host side of k_verify_service (hfv_kernels.hip): tickets 1, 2, ... go to ring slot
-// (t - 1) % kSvcRing; ticket t is posted only once ticket t - kSvcRing is done.
+// (t - 1) % kSvcRing; ticket t is posted only once ticket t - kSvcRing is done.  Ring and
+// completion words hold svc_tag | t, the tag changing with every grid, so nothing is cleared
+// between grids.
 
 }  // extern "C"
 
@@ -1197,7 +1200,7 @@ static bool svc_is_done(const hfv_ctx *ctx, uint64_t t)
 {
     const uint64_t *d = ctx->svc_host->done[(t - 1) % kSvcRing];
     for (unsigned k = 0; k < ctx->svc_grid; ++k)
-        if (__atomic_load_n(&d[k], __ATOMIC_ACQUIRE) < t) return false;
+        if (__atomic_load_n(&d[k], __ATOMIC_ACQUIRE) < (ctx->svc_tag | t)) return false;
     return true;
 }
 
@@ -1236,7 +1239,7 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
     d->bits = bits;
     d->n = n;
     d->stride = stride;
-    __atomic_store_n(&d->seq, t, __ATOMIC_RELEASE);
+    __atomic_store_n(&d->seq, ctx->svc_tag | t, __ATOMIC_RELEASE);
     ctx->svc_next = t + 1;
     if (ticket) *ticket = t;
     return 0;
@@ -1286,10 +1289,13 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
         HIP_TRY(hipHostGetDevicePointer((void **)&ctx->svc_host_dev, ctx->svc_host, 0));
         HIP_TRY(hipMalloc((void **)&ctx->svc_mirror, kSvcRing * sizeof(SvcDesc)));
         for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreate(&ctx->svc_ev[i]));
+        memset(ctx->svc_host, 0, sizeof(SvcShared));
+        HIP_TRY(hipMemsetAsync(ctx->svc_mirror, 0, kSvcRing * sizeof(SvcDesc), ctx->svc_stream));
     }
-    memset(ctx->svc_host, 0, sizeof(SvcShared));
-    // stale tickets of an earlier run must not match: the mirror starts empty
-    HIP_TRY(hipMemsetAsync(ctx->svc_mirror, 0, kSvcRing * sizeof(SvcDesc), ctx->svc_stream));
+    // a new generation: words an earlier grid left in the ring, the mirror and the completion
+    // table carry a smaller tag and never match
+    ctx->svc_tag += 1ull << 40;
+    __atomic_store_n(&ctx->svc_host->status, 0, __ATOMIC_RELEASE);
     DevState *ds;
     int rc = publish_keys(ctx, ctx->svc_stream, &ds);
     if (rc) return rc;
@@ -1299,7 +1305,7 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
     ctx->svc_next = 1;
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off, ctx->hf_off,
-                                  (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_stream, ctx->svc_ev[0],
+                                  (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream, ctx->svc_ev[0],
                                   ctx->svc_ev[1], &ctx->svc_grid);
     rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
@@ -1364,7 +1370,7 @@ int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms)
 int hfv_service_running(const hfv_ctx *ctx) { return ctx && ctx->svc_running ? 1 : 0; }
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
-// 0 loaded ring slot i's descriptor; out[64..67] = block 0 wave 0's s_memtime and
+// 0 loaded ring slot i's descriptor (i < kSvcRing); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and
 // s_memrealtime at its start and at its exit (the shader clock over the grid's life).
 int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
 {

@@ -83,12 +83,12 @@ enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 // uses ring slot b % kSvcRing; the host posts ticket t only once ticket t - kSvcRing is
 // complete, which is what lets each block cache kSvcRing descriptors in LDS without any
 // reuse check (hfv_kernels.hip, k_verify_service).
-constexpr uint32_t kSvcRing = 64;
+constexpr uint32_t kSvcRing = 256;   // batches in flight (a host hiccup of ~3 ms at 2^20 records does not starve the grid)
 constexpr uint32_t kSvcMaxBlocks = 1024;
 constexpr uint64_t kSvcStopN = ~0ull;   // descriptor n: the service exits
 struct SvcDesc {
     uint64_t recs, bits, n, stride;   // device pointers / counts of the batch
-    uint64_t seq;                     // ticket; stored last, with release
+    uint64_t seq;                     // generation tag | ticket; stored last, with release
     uint64_t pad[3];
 };
 struct SvcShared {
@@ -97,7 +97,7 @@ struct SvcShared {
     uint64_t pad[7];
     uint64_t load_clock[kSvcRing];   // diagnostics: s_memrealtime when block 0 loaded the slot
     uint64_t run_clock[4];           // diagnostics: block 0 wave 0 s_memtime/s_memrealtime at start, at exit
-    uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = t: block k's share of t is verified
+    uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
 constexpr uint64_t kSvcWatchdog = 3;    // a wave gave up waiting for its block's loader
@@ -147,8 +147,8 @@ int build_ttab_image(uint32_t *img, void *stream);
 // returns the grid size in *grid
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, void *stream, void *ev_start, void *ev_stop,
-                          unsigned *grid);
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
+                          void *ev_stop, unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

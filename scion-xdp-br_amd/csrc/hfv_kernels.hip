@@ -55,6 +55,11 @@ struct RecWords {
 
 // Unconditional loads (no branch around them, so the compiler can keep a counted vmcnt for
 // the prefetch): lanes past the end re-read the last record and are masked off later.
+// NT: non-temporal loads (records are read once per launch).  The resident service uses
+// plain, cache-allocating loads instead: a batch re-posted from the same ring slots (the
+// benchmark re-verifies one resident 64 MiB batch) is then served from the Infinity Cache
+// (measured at 2^20: +8-10 %; neutral at 2^24, where the batch does not fit).
+template <bool NT = true>
 __device__ __forceinline__ RecWords load_rec(const uint8_t *recs, uint64_t stride, uint64_t i, uint64_t last,
                                              uint32_t inf_off, uint32_t hf_off)
 {
@@ -62,11 +67,20 @@ __device__ __forceinline__ RecWords load_rec(const uint8_t *recs, uint64_t strid
     // global address space even when `recs` came out of memory (the service's descriptors),
     // so these are global_load (vmcnt only), not flat loads that also count in lgkmcnt
     const GlobalU8 *p = (const GlobalU8 *)(recs) + (i < last ? i : last) * stride;
-    u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x2 *>(p + inf_off));
-    u32x2 b = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x2 *>(p + hf_off));
+    typedef const __attribute__((address_space(1))) u32x2 *P2;
+    typedef const __attribute__((address_space(1))) uint32_t *P1;
+    u32x2 a, b;
+    if constexpr (NT) {
+        a = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
+        b = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
+        r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
+    } else {
+        a = *reinterpret_cast<P2>(p + inf_off);
+        b = *reinterpret_cast<P2>(p + hf_off);
+        r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
+    }
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
-    r.hfb = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(p + hf_off + 8));
     return r;
 }
 
@@ -625,6 +639,10 @@ struct SvcSlot {
 };
 static __shared__ SvcSlot s_svc[kSvcRing];
 static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
+// Generation tag of this service grid (kernel argument, gen << 40): the host ring, the device
+// mirror and the completion words carry tag | ticket, so words a previous grid left behind
+// never match and nothing has to be cleared between grids.
+static __shared__ uint64_t s_svc_tag;
 
 struct SvcTile {   // one claimed tile, wave-uniform
     uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + (g - base)
@@ -649,7 +667,7 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 // at the memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/).
 __device__ void svc_complete(SvcShared *host, uint32_t b)
 {
-    __hip_atomic_store(&host->done[b % kSvcRing][blockIdx.x], (uint64_t)b + 1, __ATOMIC_RELAXED,
+    __hip_atomic_store(&host->done[b % kSvcRing][blockIdx.x], s_svc_tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -667,9 +685,10 @@ __device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks)
         const uint32_t slot = b % kSvcRing;
         SvcDesc *h = &host->desc[slot];
         bool idle = false;
-        if (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)b + 1) {
+        const uint64_t want = s_svc_tag | ((uint64_t)b + 1);
+        if (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)b + 1) {
+            while (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
                     idle = true;
                     break;
@@ -696,7 +715,7 @@ __device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks)
         __hip_atomic_store(&m->n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&m->stride, stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&m->seq, (uint64_t)b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&m->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n == kSvcStopN) return;
     }
 }
@@ -710,10 +729,11 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
     const uint32_t slot = b % kSvcRing;
     SvcDesc *d = &mir[slot];
     bool stop = false;
-    if (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint64_t)b + 1) {
+    const uint64_t want = s_svc_tag | ((uint64_t)b + 1);
+    if (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
         if (!blocking) return false;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint64_t)b + 1) {
+        while (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000000ull) {
                 __hip_atomic_store(&host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 stop = true;
@@ -858,7 +878,7 @@ template <int KEYSEL, int TAB>
 __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__restrict__ tab,
                                                          const uint32_t *__restrict__ ttab_img, SvcShared *host,
                                                          SvcDesc *mir, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t idle_ticks)
+                                                         uint64_t idle_ticks, uint64_t tag)
 {
     const uint32_t lane = threadIdx.x & 63;
     UniformKey ukey(tab);
@@ -866,6 +886,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         s_svc_next = 0;
         s_svc_loaded = 0;
         s_svc_lock = 0;
+        s_svc_tag = tag;
     }
     fill_ttab_dma_issue<TAB, 1024>(ttab_img);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -906,7 +927,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if constexpr (HFV_SVC_ACQ == 2)
             return load_rec_sys((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
         else
-            return load_rec((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
+            return load_rec<false>((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
     };
     RecWords rc = load(cur);
     svc_prefetch(host, mir, idle_ticks, lane, cur.b);
@@ -966,8 +987,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
 
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, void *stream, void *ev_start, void *ev_stop,
-                          unsigned *grid_out)
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
+                          void *ev_stop, unsigned *grid_out)
 {
     auto k = keysel == HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_IFID, 2> : k_verify_service<HFV_KEYSEL_ZERO, 4>;
     const char *ge = getenv("HFV_SVC_GRID");   // experiments only: fewer blocks than CUs
@@ -976,7 +997,7 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     *grid_out = grid;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, host, mir, inf_off, hf_off,
-                          idle_ticks);
+                          idle_ticks, tag);
     return (int)hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ MAX_KEYS = 256
 REC_INF_OFF = 40
 REC_HF_OFF = 48
 REC_SIZE = 64
+SVC_RING = 256   # resident-service descriptor ring (kSvcRing, csrc/hfv_internal.h)
 BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic HBM bytes per verified record
 
 
@@ -341,12 +342,12 @@ class Ctx:
     def service_shader_mhz(self):
         """Diagnostic: block 0's shader clock over the last service grid's life (s_memtime
         against the 100 MHz s_memrealtime), or None."""
-        clk = (ctypes.c_uint64 * 68)()
+        clk = (ctypes.c_uint64 * (SVC_RING + 4))()
         L = lib()
         L.hfv_debug_service_clocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         if L.hfv_debug_service_clocks(self._h, clk) != 0:
             return None
-        t0, r0, t1, r1 = (int(x) for x in clk[64:68])
+        t0, r0, t1, r1 = (int(x) for x in clk[SVC_RING:SVC_RING + 4])
         return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
 
     @property

@@ -35,11 +35,11 @@ for rep in range(3):
     for t in tickets:
         ctx.service_wait(t, 20000)
         done.append(time.perf_counter() - t0)
-    clk = np.zeros(68, dtype=np.uint64)
+    clk = np.zeros(hfv.SVC_RING + 4, dtype=np.uint64)
     L.hfv_debug_service_clocks(ctx._h, clk.ctypes.data)
     grid = ctx.service_stop()
     L.hfv_debug_service_clocks(ctx._h, clk.ctypes.data)   # exit stamps are written at stop
-    rc = [int(x) for x in clk[64:68]]
+    rc = [int(x) for x in clk[hfv.SVC_RING:hfv.SVC_RING + 4]]
     shader_mhz = (rc[2] - rc[0]) / ((rc[3] - rc[1]) / 100.0) if rc[3] > rc[1] else None
     done_us = np.array(done) * 1e6
     gaps = np.diff(done_us)

@@ -74,7 +74,7 @@ def test_service_ragged_batches_vs_oracle(ctx, keysel):
     junk = rng.random(len(recs)) < 0.2
     recs[junk] = rng.integers(0, 256, size=(int(junk.sum()), 64), dtype=np.uint8)
     d = dev(recs)
-    sizes = [0, 1, 2, 63, 64, 65, 127, 255, 4097, 16385, 40000] * 9   # 99 batches > 64-slot ring
+    sizes = [0, 1, 2, 63, 64, 65, 127, 255, 4097, 16385, 40000] * 27   # 297 batches > 256-slot ring
     bufs = [new_bits(n, fill=-1) for n in sizes]
     torch.cuda.synchronize()
     outs = []

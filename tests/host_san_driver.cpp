@@ -1,5 +1,6 @@
 // The product's host-side C++ (csrc/hfv_aes_host.cpp: the aes.h API the control plane
-// links; csrc/hfv_keymap.cpp and csrc/hfv_statsmap.cpp: the pinned key and counter maps)
+// links, verify_hop_field's scalar form and the br-loader base64 key decode;
+// csrc/hfv_keymap.cpp and csrc/hfv_statsmap.cpp: the pinned key and counter maps)
 // built with AddressSanitizer + UBSan and exercised here (tests/test_sanitize.py).  Expected
 // values: FIPS-197 appendix B and the RFC 4493 CMAC vectors, which the reference's
 // aes_test.cpp:33-245 also checks (tests/golden/kat.json).  Any failure aborts.
@@ -87,6 +88,25 @@ int main()
         if (len <= AES_CMAC_NO_LOOP_MAX_BYTES) CHECK(!memcmp(m1.b, m2.b, 16));
         free(heap);
     }
+
+    // ---- verify_hop_field's scalar form and the br-loader key decode ----------------------
+    // the BR key convention (run_tests:113) and a hop-field macinput whose tag starts
+    // a6 40 53 45 fa 79 (SURVEY 8c golden sample, OpenSSL-checked)
+    aes_key bk;
+    CHECK(hfv_decode_key_b64("MTExMTExMTExMTExMTExMQ==", &bk) == 0);
+    for (int i = 0; i < 16; ++i) CHECK(bk.b[i] == '1');
+    CHECK(hfv_decode_key_b64("MTEx", &bk) != 0);
+    hop_key bhk;
+    aes_key_expansion(&bk, &bhk.key);
+    aes_block bsub[2];
+    aes_cmac_subkeys(&bhk.key, bsub);
+    bhk.subkey = bsub[0];
+    macinput mi;
+    hex("000012345f5e1000003f000100020000", reinterpret_cast<uint8_t *>(&mi), 16);
+    const uint64_t expected = 0x79fa455340a6ull;   // LE u64 of tag bytes 0..5
+    CHECK(hfv_verify_macinput(&mi, expected, &bhk) == 1);
+    CHECK(hfv_verify_macinput(&mi, expected ^ 1, &bhk) == 0);
+    CHECK(hfv_verify_macinput(&mi, expected, nullptr) == 0);   // missing key fails closed
 
     // ---- pinned key map and counter map ---------------------------------------------------
     if (!getenv("HFV_PIN_DIR")) {   // the test passes its own temporary directory

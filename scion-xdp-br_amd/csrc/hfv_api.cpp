@@ -1259,8 +1259,12 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;
     if (kernel_ms) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
-    // an idle exit is clean unless it left a posted batch unverified (batches may complete
-    // out of order; only the newest kSvcRing can still be open)
+    // A grid that left on the stop descriptor verified every batch before it (each block
+    // reaches the stop only after its share of all earlier batches).  An idle or watchdog
+    // exit is clean unless it left a posted batch unverified (batches may complete out of
+    // order; only the newest kSvcRing can still be open): scan those.  (The scan reads
+    // kSvcRing x grid completion words, ~0.1 ms; it is not paid on a normal stop.)
+    if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) return 0;
     for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t)
         if (!svc_is_done(ctx, t))
             return fail(-ETIMEDOUT, "verify service exited on its idle timeout before ticket %llu",

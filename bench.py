@@ -346,7 +346,7 @@ def run_br(args, rank, world, local):
         "config": {"workload": f"config 4: {n} frames per GPU through hfv_br_process as br1-ff00_0_1-1",
                    "frames_per_gpu": n, "slot_bytes": BR_SLOT, "parallelism": f"batch-sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_br_process",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("br", n), "kernel": "k_br_process",
                      "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(ks[len(ks) // 2], 5),
                      "algorithmic_bytes_per_frame": round(alg, 2),
                      "kernel_mpkts": round(n / k_mean / 1e3, 1)},

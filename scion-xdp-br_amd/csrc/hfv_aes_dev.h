@@ -25,6 +25,12 @@ static __constant__ uint32_t c_t0[256] = {T0V64(0), T0V64(64), T0V64(128), T0V64
 // four (128 KiB) and needs no rotation.
 static __shared__ uint32_t s_tab64[16384];
 static __shared__ uint32_t s_tab128[32768];
+// TAB = 3: T0/T1 with 16 lane copies in 32 KiB for kernels where AES is a small part of the
+// work and LDS is needed for other things (the router kernel): byte address
+//   (x << 7) | (t << 6) | ((L & 15) << 2)
+// formed with a shift instead of v_perm (the state byte lands at bit 7), at the cost of
+// two-way bank conflicts (lanes L and L + 16 share a copy).
+static __shared__ uint32_t s_tab32[8192];
 static __shared__ uint4 s_keys[kDevKeyRows * HFV_MAX_KEYS];   // 48 KiB, round-major
 static __shared__ uint32_t s_valid[8];
 static __shared__ uint32_t s_next_tile;   // DYN: the block's tile queue head
@@ -51,6 +57,14 @@ __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l
 template <int TAB>
 __device__ __forceinline__ void fill_ttab()
 {
+    if constexpr (TAB == 3) {
+#pragma unroll 4
+        for (int e = threadIdx.x; e < 8192; e += blockDim.x) {
+            uint32_t t = c_t0[e >> 5];
+            s_tab32[e] = ((e >> 4) & 1) ? __builtin_amdgcn_alignbit(t, t, 24) : t;   // T1 = rotl8(T0)
+        }
+        return;
+    }
     constexpr int kDwords = TAB == 4 ? 32768 : 16384;
     uint32_t *dst = TAB == 4 ? s_tab128 : s_tab64;
 #pragma unroll 4
@@ -117,6 +131,10 @@ template <int TAB, int K>
 __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l)
 {
     static_assert(K >= 0 && K < 4, "state byte");
+    if constexpr (TAB == 3) {
+        const uint32_t a3 = (__builtin_amdgcn_ubfe(w, 8 * K, 8) << 7) | base;
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab32) + a3);
+    }
     const uint32_t a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
     const char *t = TAB == 4 ? reinterpret_cast<const char *>(s_tab128) : reinterpret_cast<const char *>(s_tab64);
     return *reinterpret_cast<const uint32_t *>(t + a);
@@ -232,7 +250,7 @@ struct UniformKey {          // slot 0 for every lane, kept in SGPRs
     template <int TAB>
     __device__ __forceinline__ uint4 rk(int r) const
     {
-        if constexpr (TAB == 2) {
+        if constexpr (TAB == 2 || TAB == 3) {
             return k[r];
         } else {   // undo the image's rotation; uniform operands, so these stay scalar
             auto u = [](uint32_t x) { return (x >> 16) | (x << 16); };
@@ -286,6 +304,17 @@ __device__ __forceinline__ Lane lane_bases()
     l.b1 = l.b0 | 0x80u;
     l.b2 = l.b0 | 0x10000u;
     l.b3 = l.b1 | 0x10000u;
+    return l;
+}
+
+// Lane bases for the TAB = 3 layout (b0: T0, b1: T1; b2/b3 unused: T2/T3 are rotations).
+__device__ __forceinline__ Lane lane_bases3()
+{
+    Lane l = lane_bases();
+    l.b0 = (threadIdx.x & 15) << 2;
+    l.b1 = l.b0 | 0x40u;
+    l.b2 = l.b0;
+    l.b3 = l.b1;
     return l;
 }
 

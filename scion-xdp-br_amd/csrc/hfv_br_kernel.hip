@@ -12,13 +12,15 @@
 // with the reference's quirks kept (listed in oracle/hfv_br_oracle.c, the CPU checker).
 // bpf_fib_lookup is replaced by the static next-hop table of the installed hfv_br_config.
 //
-// Mapping: one lane per frame, a persistent grid with one 1024-thread block per CU.  Each
-// block stages the AES round tables (64 KiB, LDS-DMA from the ctx image), the router tables
-// (~10 KiB) and its verdict counters (11 KiB) in LDS.  Frames are read and patched in place in
-// HBM through byte loads/stores of just the header fields the parser touches; payload bytes
-// are never read.  At most one hop field is checked per frame (ingress from a neighbour AS
-// or egress of a packet from the own AS), with the record-verify kernel's AES code (slot-0
-// key in SGPRs, conflict-free replicated T-tables).
+// Mapping: one lane per frame, a persistent grid with one block per CU (768 threads when the
+// headers are staged, 1024 otherwise).  Each block builds the AES round tables in LDS (T0/T1,
+// 16 replicas, 32 KiB: AES is a small part of the router's work, so LDS goes to header rows),
+// and stages the router tables (~10 KiB), its verdict counters (11 KiB) and, in the staged
+// variant, the first 128 bytes of each frame of its waves' tiles.  Frames are patched in place
+// in HBM through byte stores of just the header fields the rewrite touches; payload bytes are
+// never read.  At most one hop field is checked per frame (ingress from a neighbour AS or
+// egress of a packet from the own AS), with the record-verify kernel's AES code (slot-0 key
+// in SGPRs).
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdlib.h>
@@ -36,7 +38,7 @@ static __shared__ unsigned long long s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_C
 // writes and the per-lane reads bank-conflict free), for up to kBrStageWaves waves per block.
 constexpr int kBrWin = 128;
 constexpr int kBrRow = kBrWin / 4 + 1;
-constexpr int kBrStageWaves = 8;
+constexpr int kBrStageWaves = 12;
 static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 
 // enum xdp_action and enum verdict (br/src/bpf/common.h:38-70)
@@ -615,7 +617,7 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
             // slot-0 key (xdp.c:82) through the scalar cache, only where a hop field is checked
             const UniformKey ukey(keys);
             uint32_t t0, t1;
-            cmac48_macinput<2>(k.mi, ukey, l, t0, t1);
+            cmac48_macinput<3>(k.mi, ukey, l, t0, t1);
             ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
         }
         if (!ok) v = V_INVALID_HF;
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
 {
     static_assert(WIN == 0 || (WIN == kBrWin && BLOCK / 64 <= kBrStageWaves), "staging geometry");
     constexpr int C = WIN > 0 ? WIN / 16 : 1;   // 16-byte chunks per frame
-    fill_ttab_dma<2>(ttab_img);
+    fill_ttab<3>();   // 32 KiB (AES is a small part of the router's work; LDS goes to header rows)
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(&st->br);
         uint4 *dst = reinterpret_cast<uint4 *>(&s_br);
@@ -652,15 +654,16 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     if constexpr (STATS)
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) s_stats[e] = 0;
     __syncthreads();
-    const Lane l = lane_bases();
+    const Lane l = lane_bases3();
 
     const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint64_t ntiles = (n + 63) / 64, nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
     uint64_t t = (uint64_t)blockIdx.x * (BLOCK / 64) + wib;
     const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
-    // The tile's header rows and the lane's own length / ingress ifindex are fetched one tile
-    // ahead, all before anything of the current tile is loaded: vmcnt retires in issue order,
-    // so a load of the current tile issued after the prefetch would wait for the prefetch too.
+    // The tile's header rows and the lane's own length / ingress ifindex are loaded at the top
+    // of each tile, with no register prefetch of the next tile: the other waves of the CU (12
+    // in the staged launch) hide the latency, and the prefetch's extra registers pushed the
+    // 12-wave kernel into scratch spills (measured 152 us against 121 us).
     uint4 pre[C];
     uint32_t pre_len = 0, pre_ifx = 0;
     auto fetch = [&](uint64_t tt) {
@@ -677,8 +680,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         pre_len = lens[fi];
         pre_ifx = ifidx[fi];
     };
-    if (t < ntiles) fetch(t);
     for (; t < ntiles; t += nwaves) {
+        fetch(t);
         if constexpr (WIN > 0) {
             uint32_t *rows = s_hdr + wib * 64 * kBrRow;
 #pragma unroll
@@ -691,7 +694,6 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         const uint32_t len = pre_len, ifx = pre_ifx;
-        if (t + nwaves < ntiles) fetch(t + nwaves);
         uint64_t i = t * 64 + lane;
         bool dirty = false;
         if (i < n) {
@@ -751,8 +753,8 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     K k;
     int block;
     if (staged) {
-        block = 512;
-        k = stats ? k_br_process<512, true, kBrWin> : k_br_process<512, false, kBrWin>;
+        block = 768;
+        k = stats ? k_br_process<768, true, kBrWin> : k_br_process<768, false, kBrWin>;
     } else {
         block = 1024;
         k = stats ? k_br_process<1024, true, 0> : k_br_process<1024, false, 0>;

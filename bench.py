@@ -2,46 +2,67 @@
 """Headline benchmark: Mpkt/s of device-resident hop-field AES-CMAC verify on 64 B SCION
 records (BASELINE.json metric; config 2 = 2^20 records, single AS key, per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--keysel zero|ifid] [--n N]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--keysel zero|ifid] [--n N] [--rotate R]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-One process per GPU.  A "step" is one pass of the verifier over the rank's resident batch
-of n records (weak scaling: every rank verifies its own n records, no collective on the
-data path; RCCL is used only for the timing barrier and max-over-ranks).  By default
-(--mode service) the K steps are K batches posted one by one to the resident service
-(hfv_service_submit: the XDP program's counterpart, a grid that stays on the GPU), with
-starting and stopping its grid inside the timed region; --mode launch times one
-hfv_verify_records launch per step instead (both are always measured and reported:
-`service`, `per_launch`).  Rank 0 prints one JSON line.  Besides
-the contract fields it carries:
+One process per GPU.  `--gpus N` with N > 1 and no torch.distributed environment starts the
+N rank processes itself (torch.distributed.run as a CHILD process, before this process
+touches a GPU) and exits with their status.  A "step" is one batch of the rank's n records
+(weak scaling: every rank verifies its own records, no collective on the data path; the
+collective backend carries only the timing barrier, max-over-ranks and the per-rank
+report).  The rank's records sit in R distinct resident batches (default R = 8: 8 x 64 MiB =
+512 MiB, twice the 256 MiB Infinity Cache) and step k verifies batch k % R, so every step
+reads its records from HBM, not from the memory-side cache; every step writes its own
+verdict bitmap.
+
+By default (--mode service) the K steps are K batches posted to the resident service
+(hfv_service_submitv: the XDP program's counterpart, a grid that stays on the GPU), with the
+grid launch, its table fill and its drain inside the timed region; --mode launch times one
+hfv_verify_records launch per step instead (both are always measured: `service`,
+`per_launch`).  Rank 0 prints one JSON line.  Besides the contract fields it carries:
   roofline      -- the headline kernel's algorithmic bytes (64 B read + 1/8 B verdict per
                    record) / its duration from the dispatch's own start/stop events (the
-                   service grid's lifetime over all K batches, or the mean launch), against
-                   the 8 TB/s HBM3E peak; `traffic` is the PMC-measured HBM bytes per batch
-                   from profiles/ when a matching pass exists.
+                   service grid's lifetime over all K batches), against the 8 TB/s HBM3E
+                   peak; `traffic` is the PMC-measured HBM bytes per batch of the same
+                   configuration (profiles/traffic.json), when one was measured.
+  ceilings      -- LDS lookups and VALU instructions per packet read at run time from the
+                   committed PMC summary of this configuration, and the LDS-issue bound at
+                   the shader clock the grid ran at.
   cpu_baseline  -- the reference's own aes.c soft path (oracle/_ref, built from
-                   /root/reference) over a sample of the same records on this host's cores,
-                   verdicts cross-checked against the GPU bitmap.
-  hbm_resident  -- the same kernel on 2^24 records (1 GiB > 256 MiB Infinity Cache).
-  host_e2e      -- rate including H2D/D2H through pinned staging (hfv_verify_records_host).
+                   /root/reference) over the same records on this host's cores (median of
+                   >= 5 timed passes), verdicts cross-checked against the GPU bitmap; 1-core
+                   and AES-NI figures beside it.
+  config3       -- the same measurement with 256 ingress-interface keys (KEYSEL_IFID).
+  config4       -- the full border-router path (hfv_br_process), see --workload br.
+  hbm_resident / mall_resident -- one 2^24-record batch (1 GiB) / one 2^20 batch re-posted
+                   (Infinity-Cache resident), for comparison.
+  host_e2e      -- rate including H2D/D2H (records in host memory), on every rank, the
+                   rank's host threads on its GPU's NUMA node.
 
     python bench.py --workload br [--n 1048576] [--steps 10]
 
-runs config 4 instead: the full border-router per-packet path (hfv_br_process: parse,
-AS ingress/egress, next hop, rewrite, MAC check, counters) as BR 1 of the reference test
+runs config 4 alone: the full border-router per-packet path (hfv_br_process: parse, AS
+ingress/egress, next hop, rewrite, MAC check, counters) as BR 1 of the reference test
 topology, over n frames of 64..1500 B in 2 KiB slots (PTF scenario traffic, 1/16 with a
 corrupted hop-field MAC).  Frames are rewritten in place, so each timed step gets its own
 pristine copy of the batch (K copies resident in HBM, made before the timed region).
 
     python bench.py --workload br-host [--n 1048576] [--steps 5] [--window 256]
 
-runs config 5: the same frames start and end in (registered) host memory; per step one
-hfv_br_process_host call moves the header windows over PCIe, processes them and writes the
-rewritten windows back.  Each step's input is restored (untimed) before it runs.
+runs config 5's router leg: the same frames start and end in (registered) host memory; per
+step one hfv_br_process_host call moves the header windows over PCIe, processes them and
+writes the rewritten windows back.
+
+    python bench.py --dry-run --gpus 2
+
+checks the launcher alone: N gloo ranks on the CPU, no GPU work, the line reports n_gpus.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -49,16 +70,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "scion-xdp-br_amd"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-import scion_hfv as hfv  # noqa: E402
 
 SEED_RECORDS = 0x5C100001
 SEED_KEYS = 0x5C100100
 KEY_1111 = b"1111111111111111"   # br/test/run_tests:113
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic bytes per verified record
 M64 = (1 << 64) - 1
+# committed PMC summary of the headline configuration (scripts/pmc_round.sh ... svc rot)
+PMC_SUMMARY = {"zero": "profiles/r02/pmc_svc_zero/summary.json", "ifid": "profiles/r02/pmc_svc_ifid/summary.json"}
+METRIC = "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets"
 
 
 def splitmix_at(seed, k):
@@ -75,7 +96,7 @@ def key_table_256(seed=SEED_KEYS):
     return bytes(out)
 
 
-def expected_pass_count(n, first_index):
+def corrupted(n, first_index=0):
     """Generator truth: record i is corrupted iff splitmix draw 4i+2 & 15 == 0."""
     i = np.arange(first_index, first_index + n, dtype=np.uint64)
     with np.errstate(over="ignore"):
@@ -83,7 +104,11 @@ def expected_pass_count(n, first_index):
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
-    return int(((z & np.uint64(15)) != 0).sum())
+    return (z & np.uint64(15)) == 0
+
+
+def expected_pass_count(n, first_index):
+    return int(n - corrupted(n, first_index).sum())
 
 
 def popcount(bits_t):
@@ -91,7 +116,94 @@ def popcount(bits_t):
     return int(np.unpackbits(b).sum())
 
 
-def make_ctx(device, keysel):
+# ---- launcher --------------------------------------------------------------------------------
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """Start args.gpus rank processes (torch.distributed.run, one rank per GPU) as a child
+    process and return its exit status.  Nothing in this process has touched a GPU."""
+    # torch.distributed.run reads abbreviations of its own options anywhere on the line
+    # (`--n` would match --nnodes): pass the record count under its long name
+    fwd = [("--records" + a[3:]) if a == "--n" or a.startswith("--n=") else a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + fwd
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+class World:
+    """The rank's place in the job and the timing collectives (barrier, max, gather)."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.size = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = args.dry_run
+        self.backend = "gloo" if args.dry_run else args.dist_backend
+        self.device = self.local if not args.same_device else 0
+        if not self.dry:
+            torch.cuda.set_device(self.device)
+        if self.size > 1:
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
+            else:
+                dist.init_process_group("gloo")
+        if self.size != args.gpus and self.rank == 0:
+            print(f"bench: --gpus {args.gpus} but the job has {self.size} ranks; reporting {self.size}",
+                  file=sys.stderr)
+
+    def sync(self):
+        if not self.dry:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.size > 1:
+            self.dist.barrier()
+
+    def gather(self, x):
+        """Every rank's float x (rank order) on every rank."""
+        if self.size == 1:
+            return [float(x)]
+        dev = "cpu" if self.backend == "gloo" else "cuda"
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=dev)
+        out = [self.torch.zeros_like(t) for _ in range(self.size)]
+        self.dist.all_gather(out, t)
+        return [float(o.item()) for o in out]
+
+    def timed(self, steps, fn):
+        """fn() `steps` times between barrier + device sync on both sides; (max over ranks,
+        per-rank list)."""
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        self.sync()
+        self.barrier()
+        el = time.perf_counter() - t0
+        all_el = self.gather(el)
+        return max(all_el), all_el
+
+    def close(self):
+        if self.size > 1:
+            self.dist.destroy_process_group()
+
+
+# ---- measurement helpers -----------------------------------------------------------------------
+
+def make_ctx(hfv, device, keysel):
     ctx = hfv.Ctx(device)
     if keysel == hfv.KEYSEL_IFID:
         ctx.key_add_batch(0, key_table_256())
@@ -101,86 +213,125 @@ def make_ctx(device, keysel):
     return ctx
 
 
-def kernel_ms(ctx, recs, n, bits, stream, reps):
-    """Mean/median execution time of one verify launch on `stream`, from the dispatch's own
-    start/stop timestamps (hipExtLaunchKernel events, hfv_verify_records_timed)."""
-    ts = sorted(ctx.verify_records_timed(recs, n, bits, stream=stream) for _ in range(reps))
-    return float(np.mean(ts)), float(ts[len(ts) // 2])
-
-
-def timed_steps(world, steps, fn):
-    """Run fn `steps` times between barrier + device sync on both sides; max over ranks."""
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
-
-
-def ceilings(keysel):
-    """The other bounds beside HBM, per packet, from this repo's own measurements (DESIGN.md
-    section 4): LDS lookups and VALU instructions per packet (PMC SQ_INSTS_LDS/VALU x 64 /
-    records, profiles/r01/service/pmc_zero_svc), the chip's conflict-free ds_read_b32 rate
-    (scripts/ubench/valu_rate.hip) and the streaming-read rate of the same access pattern
-    without compute (scripts/ubench/stream_read.hip, 1 GiB)."""
-    lds_per_pkt = 146.2 if keysel == "zero" else None
-    lds_rate = 16.8e12
-    out = {"lds_lookups_per_pkt": lds_per_pkt, "lds_peak_lookups_per_s": lds_rate,
-           "valu_instr_per_pkt": 277.0 if keysel == "zero" else None,
-           "streaming_read_GBs": 6552.0, "streaming_read_frac": round(6552.0 / HBM_PEAK_GBS, 3),
-           "source": "profiles/r01/service/pmc_zero_svc/summary.json, profiles/r01/ubench/"}
-    if lds_per_pkt:
-        out["lds_bound_mpkts"] = round(lds_rate / lds_per_pkt / 1e6, 1)
-    out["streaming_read_bound_mpkts"] = round(6552.0e9 / hfv.BYTES_PER_PACKET / 1e6, 1)
-    return out
-
-
-def lds_bound_at_clock(keysel, mhz):
-    """The LDS-issue bound at the shader clock the service grid actually ran at (it is power
-    limited: ~2.38 GHz with 32 CUs busy, ~1.5-1.6 GHz sustained with all 256, scripts/svc_probe.py):
-    conflict-free ds_read_b32 retires 32 lanes per clock per CU."""
-    if not mhz or keysel != "zero":
-        return {}
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    # VALU: per 64-packet tile 145 v_perm_b32 (4 SIMD cycles per wave64 instruction, measured
-    # half rate) + 132 full-rate instructions (2 cycles); 4 SIMDs per CU
-    valu_cycles_per_pkt = (145 * 4 + 132 * 2) / 64.0
-    return {"service_shader_mhz": round(mhz, 1),
-            "lds_bound_mpkts_at_service_clock": round(cus * 32 * mhz * 1e6 / 146.2 / 1e6, 1),
-            "valu_bound_mpkts_at_service_clock": round(cus * 4 * mhz * 1e6 / valu_cycles_per_pkt / 1e6, 1)}
-
-
-def pmc_traffic(keysel, n, service=False):
-    """HBM bytes per launch (per batch for the resident service) measured by rocprofv3 PMC
-    passes (scripts/pmc_round.sh) for this exact configuration, committed in
-    profiles/traffic.json; None if not measured."""
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+def pmc_summary(keysel):
+    """The committed PMC summary of the headline configuration for this keysel, or None."""
     try:
-        return json.load(open(tpath))[f"{'svc:' if service else ''}{keysel}:{n}"]["hbm_bytes_per_launch"]
+        return json.load(open(os.path.join(ROOT, PMC_SUMMARY[keysel])))
     except Exception:
         return None
 
 
+def pmc_traffic(key):
+    """HBM bytes per batch/launch measured by rocprofv3 PMC passes for this exact
+    configuration (profiles/traffic.json), or None."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[key]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def ceilings(keysel, n, mhz, cus):
+    """Bounds beside HBM, per packet, read from the committed PMC summary of this
+    configuration (SQ_INSTS_LDS / SQ_INSTS_VALU are wave-instructions: x 64 lanes / records
+    per batch) and the chip's conflict-free ds_read_b32 issue rate (32 lanes per clock per
+    CU, MI355X_MICROARCH.md LDS table) at the shader clock the grid ran at."""
+    s = pmc_summary(keysel)
+    out = {"source": PMC_SUMMARY[keysel] if s else None}
+    row = (s or {}).get(str(n))
+    if not row:
+        return out
+    lds = row["SQ_INSTS_LDS"] * 64 / n
+    valu = row["SQ_INSTS_VALU"] * 64 / n
+    out.update({"lds_instr_per_pkt": round(lds, 1), "valu_instr_per_pkt": round(valu, 1)})
+    if mhz:
+        out["shader_mhz"] = round(mhz, 1)
+        out["lds_issue_bound_mpkts"] = round(cus * 32 * mhz * 1e6 / lds / 1e6, 1)
+    out["hbm_peak_bound_mpkts"] = round(HBM_PEAK_GBS * 1e9 / BYTES_PER_PACKET / 1e6, 1)
+    return out
+
+
+def service_grid(ctx, batches, steps, bitmaps, n):
+    """Start the resident service, post `steps` batches (batch k % R, bitmap k) in one
+    submitv call, stop it after the last; returns the grid's lifetime in ms."""
+    ctx.service_start()
+    ctx.service_submitv([(batches[k % len(batches)], n, bitmaps[k]) for k in range(steps)])
+    return ctx.service_stop()
+
+
+def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream, bitmap_cap=1024,
+               service=True):
+    """Resident records in `rotate` batches, launch path and service path; returns a dict."""
+    torch = W.torch
+    R = rotate
+    batches = [torch.empty((n, 64), dtype=torch.uint8, device="cuda") for _ in range(R)]
+    for i, b in enumerate(batches):
+        ctx.gen_records(b, n, SEED_RECORDS, first_index=first + i * n, stream=stream)
+    nb = max(R, min(steps, bitmap_cap))
+    bitmaps = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    expect = [expected_pass_count(n, first + i * n) for i in range(R)]
+
+    def check(k_steps):
+        for k in range(min(k_steps, nb)):
+            assert popcount(bitmaps[k]) == expect[k % R], f"bitmap {k} disagrees with generator truth"
+
+    # --- launch path: one hfv_verify_records launch (+ table fill) per batch ---
+    for k in range(max(warmup, R)):                 # >= one untimed pass over every batch
+        ctx.verify_records(batches[k % R], n, bitmaps[k % nb], stream=stream)
+    W.sync()
+    check(R)
+    step = [0]
+
+    def launch_step():
+        k = step[0]
+        ctx.verify_records(batches[k % R], n, bitmaps[k % nb], stream=stream)
+        step[0] = k + 1
+
+    launch_el, _ = W.timed(steps, launch_step)
+    ks = sorted(ctx.verify_records_timed(batches[k % R], n, bitmaps[k % nb], stream=stream)
+                for k in range(max(20, min(steps, 200))))
+    k_mean, k_med = float(np.mean(ks)), ks[len(ks) // 2]
+
+    out = {"launch_el": launch_el, "k_mean": k_mean, "k_med": k_med, "batches": batches, "bitmaps": bitmaps,
+           "svc_el": None, "per_rank_s": None, "grid_ms": None, "mhz": None}
+    if not service:
+        out["per_rank_s"] = W.gather(launch_el)
+        return out
+
+    # --- resident service: launch, table fill, K batches, drain all inside the timed region ---
+    for b in bitmaps:
+        b.zero_()
+    W.sync()
+    service_grid(ctx, batches, max(warmup, R), bitmaps, n)
+    check(R)
+    for b in bitmaps:
+        b.zero_()
+    W.sync()
+    svc = {}
+
+    def service_run():
+        svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n)
+
+    svc_el, per_rank = W.timed(1, service_run)
+    svc["mhz"] = ctx.service_shader_mhz()          # diagnostics, outside the timed region
+    check(steps)
+    out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": svc["grid_ms"], "mhz": svc["mhz"]})
+    return out
+
+
 def cpu_baseline(recs_host, keysel, gpu_bits, budget_s):
     """The reference aes.c soft path (XDP's arithmetic) timed on this host's cores over a
-    bounded sample of the same records; verdicts must equal the GPU's."""
+    bounded sample of the same records (median of >= 5 timed passes); verdicts must equal
+    the GPU's.  Threads: every CPU this process may run on, capped by OMP_NUM_THREADS when
+    the environment sets one (the GPU box gives each GPU a share of its CPUs)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import orc   # test infrastructure: only this leg of the bench may use it
 
-    raw = key_table_256() if keysel == hfv.KEYSEL_IFID else KEY_1111
+    raw = key_table_256() if keysel else KEY_1111
     hk, valid = orc.key_table(raw)
     raw256 = raw + bytes(16 * (256 - len(raw) // 16))
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(affinity, omp) if omp > 0 else affinity
     n = len(recs_host)
     use_ref = orc.reference() is not None
 
@@ -189,31 +340,54 @@ def cpu_baseline(recs_host, keysel, gpu_bits, budget_s):
             return orc.ref_verify_records(recs_host, raw256, hk, valid, keysel, nthreads=nthreads, aesni=aesni)
         return orc.verify_records(recs_host, hk, valid, keysel, nthreads=nthreads)
 
-    t0 = time.perf_counter()
-    bits1 = run(1)
-    t1c = time.perf_counter() - t0
-    reps, t_all = 0, 0.0
-    while t_all < budget_s or reps == 0:
-        t0 = time.perf_counter()
-        bitsN = run(cores)
-        t_all += time.perf_counter() - t0
-        reps += 1
-    assert np.array_equal(bits1, bitsN)
+    def rate(nthreads, aesni, reps, budget):
+        ts, bits = [], None
+        t_all = 0.0
+        while len(ts) < reps or t_all < budget:
+            t0 = time.perf_counter()
+            bits = run(nthreads, aesni)
+            dt = time.perf_counter() - t0
+            ts.append(dt)
+            t_all += dt
+            if len(ts) >= 50:
+                break
+        return n / statistics.median(ts) / 1e6, len(ts), bits
+
+    # 1-core figures on a 2^16-record slice (one pass of the soft path over 2^20 takes ~0.25 s)
+    m1 = min(n, 1 << 16)
+    sub = recs_host[:m1]
+    soft1 = [None]
+
+    def run1(aesni):
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            b = orc.ref_verify_records(sub, raw256, hk, valid, keysel, nthreads=1, aesni=aesni) if use_ref else \
+                orc.verify_records(sub, hk, valid, keysel, nthreads=1)
+            ts.append(time.perf_counter() - t0)
+            soft1[0] = b
+        return m1 / statistics.median(ts) / 1e6
+
+    one_soft = run1(0)
+    one_aesni = run1(1) if use_ref else None
+    v, reps, bitsN = rate(threads, 0, 5, budget_s)
     match = bool(np.array_equal(bitsN, gpu_bits))
-    out = {"value": round(n * reps / t_all / 1e6, 3), "unit": "Mpkt/s", "cores": cores,
-           "kind": "reference" if use_ref else "port",
-           "sample": f"{n} records of the benched batch x {reps} passes, aes_cmac soft path (aes/src/aes.c), "
-                     f"{cores} threads; 1-thread {round(n / t1c / 1e6, 3)} Mpkt/s",
-           "single_core_mpkts": round(n / t1c / 1e6, 3),
-           "verdicts_match_gpu": match}
+    out = {"value": round(v, 3), "unit": "Mpkt/s", "cores": threads, "kind": "reference" if use_ref else "port",
+           "sample": f"{n} records of the benched batch, median of {reps} timed passes, aes_cmac soft path "
+                     f"(aes/src/aes.c, what XDP executes), {threads} threads",
+           "nproc": os.cpu_count(), "affinity_cpus": affinity,
+           "threads_note": "all CPUs of the process affinity" if not omp or omp >= affinity else
+                           f"capped by OMP_NUM_THREADS={omp} (this GPU's share of the host CPUs)",
+           "single_core_mpkts": round(one_soft, 3), "verdicts_match_gpu": match}
     if use_ref:
-        t0 = time.perf_counter()
-        bitsA = run(cores, aesni=1)
-        ta = time.perf_counter() - t0
+        va, reps_a, bitsA = rate(threads, 1, 5, 0.0)
         assert np.array_equal(bitsA, bitsN)
-        out["aesni_mpkts"] = round(n / ta / 1e6, 3)
+        out["aesni_mpkts"] = round(va, 3)
+        out["aesni_single_core_mpkts"] = round(one_aesni, 3)
     return out
 
+
+# ---- config 4 / 5: the full router path ---------------------------------------------------------
 
 BR_SLOT = 2048
 BR_KINDS = ("down", "up", "core", "seg_switch")
@@ -253,117 +427,6 @@ def br_templates():
     return frames, ifis, good, abytes
 
 
-def corrupted(n, first_index=0):
-    """Same 1/16 corruption draw as the 64 B records (splitmix64 draw 4i+2 & 15 == 0)."""
-    i = np.arange(first_index, first_index + n, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        z = np.uint64(SEED_RECORDS) + (np.uint64(4) * i + np.uint64(3)) * np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z = z ^ (z >> np.uint64(31))
-    return (z & np.uint64(15)) == 0
-
-
-def br_cpu_baseline(frames_host, lens, ifidx, cfg, budget_s):
-    """The oracle border router (a scalar C restatement of xdp.c; the BPF program itself cannot
-    run here) on one host core over a sample of the same frames."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import orc   # test infrastructure: only the cpu_baseline leg may use it
-    from scion_hfv import topology as TP
-    hk = orc.hop_key(TP.KEYS[1])
-    reps, t_all, n = 0, 0.0, len(frames_host)
-    while t_all < budget_s or reps == 0:
-        work = frames_host.copy()
-        t0 = time.perf_counter()
-        a, v, e, s = orc.br_process(work, lens, ifidx, cfg, hk)
-        t_all += time.perf_counter() - t0
-        reps += 1
-    return a, {"value": round(n * reps / t_all / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-               "sample": f"{n} frames of the benched mix x {reps} passes, oracle/hfv_br_oracle.c (scalar restatement "
-                         f"of br/src/bpf/xdp.c process_packet + verify), 1 thread"}
-
-
-def run_br(args, rank, world, local):
-    from scion_hfv import topology as TP
-    n, steps = args.n, args.steps
-    if steps > 32:
-        raise SystemExit("--workload br keeps one pristine 2 KiB-slot batch per timed step in HBM: use --steps <= 32")
-    ctx = hfv.Ctx(local)
-    ctx.key_add(0, TP.KEYS[1])
-    cfg = TP.br_config("br1")
-    ctx.br_set_config(cfg)
-    stream = torch.cuda.current_stream().cuda_stream
-    frames, ifis, good, abytes = br_templates()
-    tmpl, tid, lens, _, n_good = br_batch(n, rank)
-    d_tid = torch.from_numpy(tid.astype(np.int64)).cuda()
-    master = torch.from_numpy(tmpl).cuda()[d_tid]                    # n x 2 KiB, gathered on device
-    d_len = torch.from_numpy(lens.view(np.int16)).cuda()
-    d_if = torch.from_numpy(np.array(ifis, dtype=np.int32)).cuda()[d_tid]
-    act = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    ver = torch.zeros_like(act)
-    egr = torch.zeros(n, dtype=torch.int32, device="cuda")
-    stats = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
-    alg = float(np.array(abytes)[tid].mean())
-
-    work = torch.empty_like(master)
-    for _ in range(max(1, args.warmup)):
-        work.copy_(master)
-        ctx.br_process(work, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream)
-    torch.cuda.synchronize()
-    assert int((act == 4).sum()) == n_good and int((ver == hfv.VERDICT["INVALID_HF"]).sum()) == n - n_good
-    del work
-    copies = [master.clone() for _ in range(steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for c in copies:
-        ctx.br_process(c, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ks = []
-    for c in copies[: min(steps, 10)]:
-        c.copy_(master)
-        ks.append(ctx.br_process_timed(c, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream))
-    ks.sort()
-    k_mean = float(np.mean(ks))
-    achieved = alg * n / (k_mean * 1e-3) / 1e9
-    result = {
-        "metric": "Mpkt/s full border-router per-packet path (parse + hop-field MAC verify + rewrite), "
-                  "mixed 64-1500 B frames",
-        "value": round(world * n * steps / elapsed / 1e6, 2),
-        "unit": "Mpkt/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (PTF scenario frames of the reference test topology for BR 1, 24 flows, 64-1500 B, "
-                "2 KiB slots, 1/16 corrupted MACs)",
-        "config": {"workload": f"config 4: {n} frames per GPU through hfv_br_process as br1-ff00_0_1-1",
-                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "parallelism": f"batch-sharded x{world}, no collective"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("br", n), "kernel": "k_br_process",
-                     "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(ks[len(ks) // 2], 5),
-                     "algorithmic_bytes_per_frame": round(alg, 2),
-                     "kernel_mpkts": round(n / k_mean / 1e3, 1)},
-    }
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        m = min(n, 1 << 16)
-        hf = master[:m].cpu().numpy()
-        a_cpu, result["cpu_baseline"] = br_cpu_baseline(hf, lens[:m], np.array(ifis, dtype=np.uint32)[tid[:m]],
-                                                        cfg, min(args.cpu_budget, 5.0))
-        result["cpu_baseline"]["actions_match_gpu"] = bool((a_cpu == act[:m].cpu().numpy()).all())
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
-
-
 def br_batch(n, rank):
     """Host copy of the config-4 batch: frames [n, 2 KiB], lengths, ingress ifindex, #good."""
     frames, ifis, good, abytes = br_templates()
@@ -378,13 +441,126 @@ def br_batch(n, rank):
     return tmpl, tid, lens, np.array(ifis, dtype=np.uint32)[tid], int(np.array(good)[tid].sum())
 
 
-def run_br_host(args, rank, world, local):
+def br_cpu_baseline(frames_host, lens, ifidx, cfg, budget_s):
+    """The oracle border router (a scalar C restatement of xdp.c; the BPF program itself cannot
+    run here) on one host core over a sample of the same frames."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc   # test infrastructure: only the cpu_baseline leg may use it
+    from scion_hfv import topology as TP
+    hk = orc.hop_key(TP.KEYS[1])
+    ts, n = [], len(frames_host)
+    a = None
+    while len(ts) < 5 or sum(ts) < budget_s:
+        work = frames_host.copy()
+        t0 = time.perf_counter()
+        a, v, e, s = orc.br_process(work, lens, ifidx, cfg, hk)
+        ts.append(time.perf_counter() - t0)
+        if len(ts) >= 50:
+            break
+    return a, {"value": round(n / statistics.median(ts) / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+               "sample": f"{n} frames of the benched mix, median of {len(ts)} passes, oracle/hfv_br_oracle.c "
+                         f"(scalar restatement of br/src/bpf/xdp.c process_packet + verify), 1 thread"}
+
+
+def measure_br(hfv, W, n, steps, warmup, hf_check=True):
+    """Config 4 on this rank: K pristine copies of the 2 KiB-slot batch resident in HBM, one
+    hfv_br_process launch per step.  Returns (result fields, host frames sample, ...)."""
+    from scion_hfv import topology as TP
+    torch = W.torch
+    ctx = hfv.Ctx(W.device)
+    ctx.key_add(0, TP.KEYS[1])
+    cfg = TP.br_config("br1")
+    ctx.br_set_config(cfg)
+    if not hf_check:
+        ctx.br_set_hf_check(False)
+    stream = torch.cuda.current_stream().cuda_stream
+    frames, ifis, good, abytes = br_templates()
+    tmpl, tid, lens, _, n_good = br_batch(n, W.rank)
+    d_tid = torch.from_numpy(tid.astype(np.int64)).cuda()
+    master = torch.from_numpy(tmpl).cuda()[d_tid]                    # n x 2 KiB, gathered on device
+    d_len = torch.from_numpy(lens.view(np.int16)).cuda()
+    d_if = torch.from_numpy(np.array(ifis, dtype=np.int32)).cuda()[d_tid]
+    act = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    ver = torch.zeros_like(act)
+    egr = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
+    alg = float(np.array(abytes)[tid].mean())
+    work = torch.empty_like(master)
+    for _ in range(max(1, warmup)):
+        work.copy_(master)
+        ctx.br_process(work, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream)
+    W.sync()
+    n_fwd = int((act == 4).sum())
+    if hf_check:
+        assert n_fwd == n_good and int((ver == hfv.VERDICT["INVALID_HF"]).sum()) == n - n_good
+    else:
+        assert n_fwd == n        # no MAC check: every scenario frame is forwarded
+    del work
+    copies = [master.clone() for _ in range(steps)]
+    it = iter(copies)
+    el, per_rank = W.timed(steps, lambda: ctx.br_process(next(it), BR_SLOT, d_len, d_if, n, act, ver, egr, stats,
+                                                         stream=stream))
+    ks = []
+    for c in copies[: min(steps, 10)]:
+        c.copy_(master)
+        ks.append(ctx.br_process_timed(c, BR_SLOT, d_len, d_if, n, act, ver, egr, stats, stream=stream))
+    ks.sort()
+    k_mean = float(np.mean(ks))
+    achieved = alg * n / (k_mean * 1e-3) / 1e9
+    res = {"el": el, "per_rank_s": per_rank, "k_mean": k_mean, "k_med": ks[len(ks) // 2], "alg": alg,
+           "achieved": achieved, "n_good": n_good}
+    sample = None
+    if W.rank == 0:
+        m = min(n, 1 << 16)
+        sample = (master[:m].cpu().numpy(), lens[:m], np.array(ifis, dtype=np.uint32)[tid[:m]], cfg,
+                  act[:m].cpu().numpy())
+    del copies, master
+    ctx.close()
+    return res, sample
+
+
+def run_br(args, W):
+    n, steps = args.n, args.steps
+    if steps > 32:
+        raise SystemExit("--workload br keeps one pristine 2 KiB-slot batch per timed step in HBM: use --steps <= 32")
+    import scion_hfv as hfv
+    r, sample = measure_br(hfv, W, n, steps, args.warmup, hf_check=not args.no_hf_check)
+    result = {
+        "metric": "Mpkt/s full border-router per-packet path (parse + hop-field MAC verify + rewrite), "
+                  "mixed 64-1500 B frames",
+        "value": round(W.size * n * steps / r["el"] / 1e6, 2),
+        "unit": "Mpkt/s", "n_gpus": W.size, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(r["el"] / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (PTF scenario frames of the reference test topology for BR 1, 24 flows, 64-1500 B, "
+                "2 KiB slots, 1/16 corrupted MACs)",
+        "config": {"workload": f"config 4: {n} frames per GPU through hfv_br_process as br1-ff00_0_1-1"
+                               + ("" if not args.no_hf_check else ", HF check off (ENABLE_HF_CHECK=OFF)"),
+                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "parallelism": f"batch-sharded x{W.size}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(r["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(r["achieved"] / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(f"br:{n}"),
+                     "kernel": "k_br_process", "kernel_ms_mean": round(r["k_mean"], 5),
+                     "kernel_ms_median": round(r["k_med"], 5), "algorithmic_bytes_per_frame": round(r["alg"], 2),
+                     "kernel_mpkts": round(n / r["k_mean"] / 1e3, 1)},
+        "per_rank_ms": [round(x * 1e3, 4) for x in r["per_rank_s"]],
+    }
+    if W.rank == 0 and W.size == 1 and args.cpu_budget > 0 and sample is not None:
+        hf, lens, ifx, cfg, act = sample
+        a_cpu, result["cpu_baseline"] = br_cpu_baseline(hf, lens, ifx, cfg, min(args.cpu_budget, 5.0))
+        result["cpu_baseline"]["actions_match_gpu"] = bool((a_cpu == act).all()) if not args.no_hf_check else None
+    if W.rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def run_br_host(args, W):
+    import scion_hfv as hfv
     from scion_hfv import topology as TP
     n, steps = args.n, args.steps
-    ctx = hfv.Ctx(local)
+    ctx = hfv.Ctx(W.device)
     ctx.key_add(0, TP.KEYS[1])
     ctx.br_set_config(TP.br_config("br1"))
-    tmpl, tid, lens, ifidx, n_good = br_batch(n, rank)
+    os.sched_setaffinity(0, ctx.numa_cpus())       # this GPU's host feeder runs on its NUMA node
+    tmpl, tid, lens, ifidx, n_good = br_batch(n, W.rank)
     pristine = tmpl[tid]                                   # n x 2 KiB in host memory
     frames = hfv.host_array(pristine.shape, np.uint8)
     if not args.no_register:
@@ -400,16 +576,10 @@ def run_br_host(args, rank, world, local):
     total = 0.0
     for _ in range(steps):
         frames[:, :hdr] = pristine[:, :hdr]                # restore the rewritten headers (untimed)
-        if world > 1:
-            dist.barrier()
+        W.barrier()
         t0 = time.perf_counter()
         ctx.br_process_host(frames, BR_SLOT, lens, ifidx, n, act, ver, egr, None, window=args.window)
-        dt = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        total += dt
+        total += max(W.gather(time.perf_counter() - t0))
     if not args.no_register:
         ctx.host_unregister(frames)
     path = ("DMA of %d-byte header windows (unregistered ring)" % (args.window or 256) if args.no_register else
@@ -417,130 +587,106 @@ def run_br_host(args, rank, world, local):
     result = {
         "metric": "Mpkt/s full border-router path with frames in host memory (H2D + kernel + D2H), "
                   "mixed 64-1500 B frames",
-        "value": round(world * n * steps / total / 1e6, 2), "unit": "Mpkt/s", "n_gpus": world, "steps": steps,
+        "value": round(W.size * n * steps / total / 1e6, 2), "unit": "Mpkt/s", "n_gpus": W.size, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(total / steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (the config-4 frame mix, 2 KiB slots in registered host memory)",
         "config": {"workload": f"config 5: {n} host-resident frames per GPU through hfv_br_process_host",
-                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "path": path,
-                   "parallelism": f"batch-sharded x{world}, no collective"},
+                   "frames_per_gpu": n, "slot_bytes": BR_SLOT, "path": path, "numa_node": ctx.numa_node(),
+                   "parallelism": f"batch-sharded x{W.size}, no collective"},
     }
-    if rank == 0:
+    if W.rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 200 (hf), 10 (br), 5 (br-host)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 20 (hf), 3 (br), 1 (br-host)")
-    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU (config 2: 2^20); with --strong, in total")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: --n records in total, sliced over the ranks on 64-record boundaries")
-    ap.add_argument("--keysel", choices=["zero", "ifid"], default="zero")
-    ap.add_argument("--big-n", type=int, default=1 << 24, help="HBM-resident run size (0 = skip)")
-    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
-    ap.add_argument("--no-host-e2e", action="store_true")
-    ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
-                    help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
-                         "br-host: config 5")
-    ap.add_argument("--mode", choices=["service", "launch"], default="service",
-                    help="hf headline: resident service grid (default) or one launch per batch")
-    ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")
-    ap.add_argument("--no-register", action="store_true", help="br-host: leave the ring unregistered (DMA windows)")
-    args = ap.parse_args()
-    if args.steps is None:
-        args.steps = {"hf": 200, "br": 10, "br-host": 5}[args.workload]
-    if args.warmup is None:
-        args.warmup = {"hf": 20, "br": 3, "br-host": 1}[args.workload]
+def host_leg(hfv, W, ctx, recs, n, ref_bits):
+    """PCIe-inclusive rates on this rank (every rank at once when N > 1), the rank's host
+    threads on its GPU's NUMA node: pageable records through pinned staging, and a
+    registered ring read in place by the kernel."""
+    os.sched_setaffinity(0, ctx.numa_cpus())
+    hrecs = recs.cpu().numpy()
+    hbits = np.zeros((n + 63) // 64, dtype=np.uint64)
+    ctx.verify_records_host(hrecs, n, hbits)     # warm the pinned staging
+    reps = 5
+    W.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.verify_records_host(hrecs, n, hbits)
+    th = max(W.gather((time.perf_counter() - t0) / reps))
+    assert np.array_equal(hbits, ref_bits)
+    ring = hfv.host_array((n, hfv.REC_SIZE), np.uint8)
+    ring[:] = hrecs
+    rbits = hfv.host_array(((n + 63) // 64,), np.uint64)
+    ctx.host_register(ring)
+    ctx.host_register(rbits)
+    ctx.verify_records_host(ring, n, rbits)
+    W.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.verify_records_host(ring, n, rbits)
+    tz = max(W.gather((time.perf_counter() - t0) / reps))
+    assert np.array_equal(rbits, hbits)
+    ctx.host_unregister(ring)
+    ctx.host_unregister(rbits)
+    return {"host_e2e": {"mpkts": round(W.size * n / th / 1e6, 1), "ms_per_batch": round(th * 1e3, 3),
+                         "numa_node": ctx.numa_node(),
+                         "path": "pageable host -> INF/HF gathered into 24 B pinned staging records (host threads "
+                                 "on the GPU's NUMA node) -> H2D -> kernel -> D2H -> host, 2^18-record chunks on 2 "
+                                 "streams; whole job (all ranks at once)"},
+            "host_e2e_zero_copy": {"mpkts": round(W.size * n / tz / 1e6, 1), "ms_per_batch": round(tz * 1e3, 3),
+                                   "path": "registered host ring read by the kernel over PCIe in place (PCIe moves "
+                                           "whole 64 B lines), bitmap written to registered host memory"}}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    if args.workload == "br":
-        return run_br(args, rank, world, local)
-    if args.workload == "br-host":
-        return run_br_host(args, rank, world, local)
+
+def run_dry(args, W):
+    """Launcher check without a GPU: every rank times K trivial CPU steps."""
+    x = np.arange(1 << 12, dtype=np.uint64)
+    el, per_rank = W.timed(args.steps, lambda: np.bitwise_xor.reduce(x))
+    if W.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpkt/s", "n_gpus": W.size, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "dry run: launcher check only, no GPU work", "config": {"workload": "dry run"},
+                          "per_rank_ms": [round(t * 1e3, 4) for t in per_rank], "backend": W.backend}), flush=True)
+
+
+def run_hf(args, W):
+    import scion_hfv as hfv
+    torch = W.torch
     keysel = hfv.KEYSEL_IFID if args.keysel == "ifid" else hfv.KEYSEL_ZERO
+    n = args.n
     if args.strong:   # a fixed total, sliced over the ranks (scion_hfv.shard_range)
-        first, last = hfv.shard_range(args.n, world, rank)
-        n, total = last - first, args.n
-    else:             # weak: every rank verifies its own n records
-        n, first, total = args.n, rank * args.n, world * args.n
-
-    ctx = make_ctx(local, keysel)
-    stream = torch.cuda.current_stream().cuda_stream   # int handle (0 = default stream)
-    recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
-    ctx.gen_records(recs, n, SEED_RECORDS, first_index=first, stream=stream)
-    bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
-
-    # --- launch path (hfv_verify_records: one launch + table fill per batch) ---------------
-    # W warmup steps (at least one untimed pass: the verdicts must be right before anything
-    # is timed)
-    for _ in range(max(1, args.warmup)):
-        ctx.verify_records(recs, n, bits, stream=stream)
-    torch.cuda.synchronize()
-    assert popcount(bits) == expected_pass_count(n, first), "verify bitmap disagrees with generator truth"
-    launch_elapsed = timed_steps(world, args.steps, lambda: ctx.verify_records(recs, n, bits, stream=stream))
-    k_mean, k_med = kernel_ms(ctx, recs, n, bits, stream, max(20, min(args.steps, 200)))
-
-    # --- resident service (hfv_service_*: persistent grid, host descriptor ring) ----------
-    # The timed region starts the grid, posts the K batches one by one and stops it, so the
-    # launch, the table fill and the drain are all inside it.
-    bits.zero_()
-    torch.cuda.synchronize()
-    for _ in range(max(1, args.warmup)):
-        ctx.service_submit(recs, n, bits)
-    ctx.service_stop()
-    assert popcount(bits) == expected_pass_count(n, first), "service bitmap disagrees with generator truth"
-    svc = {}
-
-    def service_run():
-        ctx.service_start()
-        for _ in range(args.steps):
-            ctx.service_submit(recs, n, bits)
-        svc["grid_ms"] = ctx.service_stop()
-
-    svc_elapsed = timed_steps(world, 1, service_run)
-    svc["shader_mhz"] = ctx.service_shader_mhz()   # diagnostics, outside the timed region
-    assert popcount(bits) == expected_pass_count(n, first)
-    headline = args.mode
-    elapsed = svc_elapsed if headline == "service" else launch_elapsed
-
-    bytes_per_launch = hfv.BYTES_PER_PACKET * n
+        a, b = hfv.shard_range(args.n, W.size, W.rank)
+        n, total = b - a, args.n
+        first = a * args.rotate
+    else:             # weak: every rank verifies its own n records per step
+        first, total = W.rank * args.n * args.rotate, W.size * args.n
+    ctx = make_ctx(hfv, W.device, keysel)
+    stream = torch.cuda.current_stream().cuda_stream
+    cus = torch.cuda.get_device_properties(W.device).multi_processor_count
+    m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream,
+                   service=not args.launch_only)
+    headline = "launch" if args.launch_only else args.mode
+    elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
+    bytes_per_batch = BYTES_PER_PACKET * n
     if headline == "service":
-        # the grid's lifetime (dispatch start/stop events) covers all K batches
-        grid_s = svc["grid_ms"] * 1e-3
-        achieved = bytes_per_launch * args.steps / grid_s / 1e9
-        kern = {"kernel": "k_verify_service", "grid_ms": round(svc["grid_ms"], 4),
-                "batches_per_grid": args.steps, "kernel_ms_per_batch": round(svc["grid_ms"] / args.steps, 5),
-                "algorithmic_bytes_per_grid": int(bytes_per_launch * args.steps)}
+        achieved = bytes_per_batch * args.steps / (m["grid_ms"] * 1e-3) / 1e9
+        kern = {"kernel": "k_verify_service", "grid_ms": round(m["grid_ms"], 4), "batches_per_grid": args.steps,
+                "kernel_ms_per_batch": round(m["grid_ms"] / args.steps, 5),
+                "algorithmic_bytes_per_batch": int(bytes_per_batch),
+                "timing": "dispatch start/stop events of the service grid (hipExtLaunchKernel) over all K batches"}
+        traffic = pmc_traffic(f"svc:{args.keysel}:{n}:rot{args.rotate}")
     else:
-        achieved = bytes_per_launch / (k_mean * 1e-3) / 1e9
-        kern = {"kernel": "k_verify_records", "kernel_ms_mean": round(k_mean, 5),
-                "kernel_ms_median": round(k_med, 5), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
-    per_launch = {"mpkts": round(total * args.steps / launch_elapsed / 1e6, 2),
-                  "ms_per_step": round(launch_elapsed / args.steps * 1e3, 5),
-                  "kernel_ms_mean": round(k_mean, 5), "kernel_ms_median": round(k_med, 5),
-                  "kernel_mpkts": round(n / k_mean / 1e3, 1),
-                  "frac": round(bytes_per_launch / (k_mean * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    service = {"mpkts": round(total * args.steps / svc_elapsed / 1e6, 2),
-               "ms_per_step": round(svc_elapsed / args.steps * 1e3, 5), "grid_ms": round(svc["grid_ms"], 4),
-               "shader_mhz": round(svc["shader_mhz"], 1) if svc["shader_mhz"] else None}
-
-    traffic = pmc_traffic(args.keysel, n, service=headline == "service")
-
+        achieved = bytes_per_batch / (m["k_mean"] * 1e-3) / 1e9
+        kern = {"kernel": "k_verify_records", "kernel_ms_mean": round(m["k_mean"], 5),
+                "kernel_ms_median": round(m["k_med"], 5), "algorithmic_bytes_per_launch": int(bytes_per_batch)}
+        traffic = pmc_traffic(f"{args.keysel}:{n}:rot{args.rotate}")
     result = {
-        "metric": "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets",
+        "metric": METRIC,
         "value": round(total * args.steps / elapsed / 1e6, 2),
         "unit": "Mpkt/s",
-        "n_gpus": world,
+        "n_gpus": W.size,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
@@ -550,93 +696,174 @@ def main():
         "dtype": "u8",
         "data": "synthetic (64 B SCION records, splitmix64 seed 0x5C100001, 1/16 corrupted MACs; generated on device)",
         "config": {"workload": f"config {'3' if keysel else '2'}: "
-                               f"{f'{total} x 64 B records in total' if args.strong else f'{n} x 64 B records per GPU'}, "
+                               f"{f'{total} x 64 B records per step in total' if args.strong else f'{n} x 64 B records per GPU per step'}, "
                                f"{'256 ingress-interface keys (KEYSEL_IFID)' if keysel else 'single AS key'}",
                    "records_per_gpu": n, "record_bytes": 64, "keysel": args.keysel,
-                   "parallelism": f"batch-sharded x{world}, no collective"},
+                   "resident_batches_per_gpu": args.rotate,
+                   "resident_bytes_per_gpu": args.rotate * n * 64,
+                   "parallelism": f"batch-sharded x{W.size}, no collective"},
         "roofline": dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}, **kern,
                          variant=ctx.describe(),
-                         note="2^20 x 64 B = 64 MiB is Infinity-Cache resident; see hbm_resident"),
-        "ceilings": dict(ceilings(args.keysel), **lds_bound_at_clock(args.keysel, svc["shader_mhz"])),
-        "path": ("resident service: one persistent grid, the K batches posted one by one through the host "
-                 "descriptor ring (hfv_service_submit); grid launch, table fill and drain inside the timed region"
+                         note=f"step k verifies resident batch k % {args.rotate} ({args.rotate} x {n * 64 >> 20} MiB "
+                              f"per GPU > 256 MiB Infinity Cache): records are read from HBM"),
+        "ceilings": ceilings(args.keysel, n, m["mhz"], cus),
+        "path": ("resident service: one persistent grid; the K batches posted through the host descriptor ring "
+                 "(hfv_service_submitv); grid launch, table fill and drain inside the timed region"
                  if headline == "service" else "one hfv_verify_records launch per batch"),
-        "service": service,
-        "per_launch": per_launch,
+        "service": None if args.launch_only else {
+            "mpkts": round(total * args.steps / m["svc_el"] / 1e6, 2),
+            "ms_per_step": round(m["svc_el"] / args.steps * 1e3, 5), "grid_ms": round(m["grid_ms"], 4),
+            "shader_mhz": round(m["mhz"], 1) if m["mhz"] else None},
+        "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),
+                       "ms_per_step": round(m["launch_el"] / args.steps * 1e3, 5),
+                       "kernel_ms_mean": round(m["k_mean"], 5), "kernel_ms_median": round(m["k_med"], 5),
+                       "kernel_mpkts": round(n / m["k_mean"] / 1e3, 1),
+                       "frac": round(bytes_per_batch / (m["k_mean"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "per_rank_ms": {"min": round(min(m["per_rank_s"]) * 1e3, 4), "max": round(max(m["per_rank_s"]) * 1e3, 4),
+                        "all": [round(x * 1e3, 4) for x in m["per_rank_s"]]},
     }
+    recs0, bits0 = m["batches"][0], m["bitmaps"][0]
+    extras = W.size == 1 and not args.no_extras
 
-    if rank == 0 and world == 1 and args.big_n:
+    if extras:   # the same batch re-posted: served from the Infinity Cache (diagnostic)
+        for b in m["bitmaps"]:
+            b.zero_()
+        W.sync()
+        g = service_grid(ctx, [recs0], args.steps, m["bitmaps"], n)
+        result["mall_resident"] = {"records": n, "service_ms_per_batch": round(g / args.steps, 5),
+                                   "service_mpkts": round(n * args.steps / g / 1e3, 1),
+                                   "service_frac": round(bytes_per_batch * args.steps / (g * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "note": "one 64 MiB batch re-posted K times: Infinity-Cache bandwidth, not HBM"}
+        W.sync()
+        assert popcount(m["bitmaps"][0]) == expected_pass_count(n, first)
+
+    if extras and args.big_n:
         nb = args.big_n
         big = torch.empty((nb, 64), dtype=torch.uint8, device="cuda")
         ctx.gen_records(big, nb, SEED_RECORDS, first_index=0, stream=stream)
-        bbits = torch.zeros((nb + 63) // 64, dtype=torch.int64, device="cuda")
+        bbits = [torch.zeros((nb + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(4)]
         for _ in range(3):
-            ctx.verify_records(big, nb, bbits, stream=stream)
-        torch.cuda.synchronize()
-        assert popcount(bbits) == expected_pass_count(nb, 0)
-        bm, bmed = kernel_ms(ctx, big, nb, bbits, stream, 20)
-        ach = hfv.BYTES_PER_PACKET * nb / (bm * 1e-3) / 1e9
-        # the same batch through the resident service, 10 batches per grid
-        bbits.zero_()
-        ctx.service_start()
-        for _ in range(10):
-            ctx.service_submit(big, nb, bbits)
-        sg = ctx.service_stop()
+            ctx.verify_records(big, nb, bbits[0], stream=stream)
+        W.sync()
+        assert popcount(bbits[0]) == expected_pass_count(nb, 0)
+        ks = sorted(ctx.verify_records_timed(big, nb, bbits[0], stream=stream) for _ in range(10))
+        bm = float(np.mean(ks))
+        ach = BYTES_PER_PACKET * nb / (bm * 1e-3) / 1e9
+        for b in bbits:
+            b.zero_()
+        W.sync()
+        sg = service_grid(ctx, [big], 4, bbits, nb)
         smhz = ctx.service_shader_mhz()
-        assert popcount(bbits) == expected_pass_count(nb, 0)
-        sach = hfv.BYTES_PER_PACKET * nb * 10 / (sg * 1e-3) / 1e9
+        for b in bbits:
+            assert popcount(b) == expected_pass_count(nb, 0)
+        sach = BYTES_PER_PACKET * nb * 4 / (sg * 1e-3) / 1e9
         result["hbm_resident"] = {"records": nb, "kernel_ms_mean": round(bm, 4), "mpkts": round(nb / bm / 1e3, 1),
                                   "achieved_GBs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                                  "traffic": pmc_traffic(args.keysel, nb),
-                                  "service_ms_per_batch": round(sg / 10, 4),
-                                  "service_mpkts": round(nb * 10 / sg / 1e3, 1),
+                                  "traffic": pmc_traffic(f"{args.keysel}:{nb}"),
+                                  "service_ms_per_batch": round(sg / 4, 4),
+                                  "service_mpkts": round(nb * 4 / sg / 1e3, 1),
                                   "service_frac": round(sach / HBM_PEAK_GBS, 4),
-                                  "service_traffic": pmc_traffic(args.keysel, nb, service=True),
+                                  "service_traffic": pmc_traffic(f"svc:{args.keysel}:{nb}"),
                                   "service_shader_mhz": round(smhz, 1) if smhz else None}
         del big, bbits
 
-    if rank == 0 and world == 1 and not args.no_host_e2e:
-        hrecs = recs.cpu().numpy()
-        hbits = np.zeros((n + 63) // 64, dtype=np.uint64)
-        ctx.verify_records_host(hrecs, n, hbits)     # warm the pinned staging
-        reps = 5
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ctx.verify_records_host(hrecs, n, hbits)
-        th = (time.perf_counter() - t0) / reps
-        assert np.array_equal(hbits, bits.cpu().numpy().view(np.uint64))
-        result["host_e2e"] = {"mpkts": round(n / th / 1e6, 1), "ms_per_batch": round(th * 1e3, 3),
-                              "path": "pageable host -> INF/HF gathered into 24 B pinned staging records (host threads) -> H2D -> "
-                                      "kernel -> D2H -> host, 2^18-record chunks on 2 streams"}
-        # the same batch in a registered (pinned, mapped) ring: the kernel reads the records'
-        # INF/HF words across PCIe in place and writes the registered bitmap in place
-        ring = hfv.host_array((n, hfv.REC_SIZE), np.uint8)
-        ring[:] = hrecs
-        rbits = hfv.host_array(((n + 63) // 64,), np.uint64)
-        ctx.host_register(ring)
-        ctx.host_register(rbits)
-        ctx.verify_records_host(ring, n, rbits)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ctx.verify_records_host(ring, n, rbits)
-        tz = (time.perf_counter() - t0) / reps
-        assert np.array_equal(rbits, hbits)
-        ctx.host_unregister(ring)
-        ctx.host_unregister(rbits)
-        result["host_e2e_zero_copy"] = {"mpkts": round(n / tz / 1e6, 1), "ms_per_batch": round(tz * 1e3, 3),
-                                        "path": "registered host ring read by the kernel over PCIe in place (grid-stride "
-                                                "tiles; PCIe moves whole 64 B lines), bitmap written to registered host memory"}
+    ref_bits = bits0.cpu().numpy().view(np.uint64).copy()
+    if extras and keysel == hfv.KEYSEL_ZERO:   # config 3 beside the config-2 headline
+        ctx3 = make_ctx(hfv, W.device, hfv.KEYSEL_IFID)
+        m3 = measure_hf(hfv, W, ctx3, "ifid", n, first, args.rotate, args.steps, args.warmup, stream)
+        a3 = bytes_per_batch * args.steps / (m3["grid_ms"] * 1e-3) / 1e9
+        result["config3"] = {"workload": f"config 3: {n} x 64 B records per GPU per step, 256 ingress-interface "
+                                         "keys (KEYSEL_IFID), same rotation and timing as the headline",
+                             "mpkts": round(total * args.steps / m3["svc_el"] / 1e6, 2),
+                             "ms_per_step": round(m3["svc_el"] / args.steps * 1e3, 5),
+                             "grid_ms": round(m3["grid_ms"], 4), "frac": round(a3 / HBM_PEAK_GBS, 4),
+                             "per_launch_mpkts": round(total * args.steps / m3["launch_el"] / 1e6, 2),
+                             "shader_mhz": round(m3["mhz"], 1) if m3["mhz"] else None,
+                             "ceilings": ceilings("ifid", n, m3["mhz"], cus)}
+        del m3
+        ctx3.close()
 
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        result["cpu_baseline"] = cpu_baseline(recs.cpu().numpy(), keysel, bits.cpu().numpy().view(np.uint64),
-                                              args.cpu_budget)
+    if not args.no_host_e2e:
+        result.update(host_leg(hfv, W, ctx, recs0, n, ref_bits))
 
-    if rank == 0:
+    if extras and args.br_n:
+        W.sync()
+        r4, sample = measure_br(hfv, W, args.br_n, 5, 2)
+        r4off, _ = measure_br(hfv, W, args.br_n, 5, 2, hf_check=False)
+        result["config4"] = {"workload": f"config 4: {args.br_n} mixed 64-1500 B frames (2 KiB slots) through "
+                                         "hfv_br_process as br1 of the reference test topology",
+                             "mpkts": round(args.br_n * 5 / r4["el"] / 1e6, 2),
+                             "kernel_ms_mean": round(r4["k_mean"], 4),
+                             "kernel_mpkts": round(args.br_n / r4["k_mean"] / 1e3, 1),
+                             "frac": round(r4["achieved"] / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes_per_frame": round(r4["alg"], 2),
+                             "traffic": pmc_traffic(f"br:{args.br_n}"),
+                             "hf_check_off_kernel_ms_mean": round(r4off["k_mean"], 4),
+                             "hf_check_off_mpkts": round(args.br_n * 5 / r4off["el"] / 1e6, 2),
+                             "hf_check_share": round(1 - r4off["k_mean"] / r4["k_mean"], 3),
+                             "note": "hf_check_off = the reference's ENABLE_HF_CHECK=OFF build (br/CMakeLists.txt:8,"
+                                     "48-64); hf_check_share = the part of the kernel time the MAC check costs"}
+
+    if W.rank == 0 and W.size == 1 and args.cpu_budget > 0:
+        result["cpu_baseline"] = cpu_baseline(recs0.cpu().numpy(), keysel, ref_bits, args.cpu_budget)
+
+    if W.rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None, help="default 200 (hf), 10 (br), 5 (br-host)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 20 (hf), 3 (br), 1 (br-host)")
+    ap.add_argument("--records", "--n", dest="n", type=int, default=1 << 20, help="records per GPU per step (config 2: 2^20); with --strong, in total")
+    ap.add_argument("--rotate", type=int, default=8,
+                    help="resident batches per GPU; step k verifies batch k %% R (8 x 64 MiB > the 256 MiB Infinity Cache)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --n records in total per step, sliced over the ranks on 64-record boundaries")
+    ap.add_argument("--keysel", choices=["zero", "ifid"], default="zero")
+    ap.add_argument("--big-n", type=int, default=1 << 24, help="HBM-resident single-batch run size (0 = skip)")
+    ap.add_argument("--br-n", type=int, default=1 << 20, help="config-4 leg frames (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
+    ap.add_argument("--no-host-e2e", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (no config 3/4, 2^24, MALL legs)")
+    ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
+                    help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
+                         "br-host: config 5 router leg")
+    ap.add_argument("--mode", choices=["service", "launch"], default="service",
+                    help="hf headline: resident service grid (default) or one launch per batch")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="measure the launch path only (ranks sharing one GPU cannot each hold a service grid)")
+    ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")
+    ap.add_argument("--no-register", action="store_true", help="br-host: leave the ring unregistered (DMA windows)")
+    ap.add_argument("--no-hf-check", action="store_true", help="br: the ENABLE_HF_CHECK=OFF router")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (launcher rehearsal on 1 GPU; gloo)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher check: gloo ranks, no GPU work")
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = {"hf": 200, "br": 10, "br-host": 5}[args.workload]
+    if args.warmup is None:
+        args.warmup = {"hf": 20, "br": 3, "br-host": 1}[args.workload]
+    if args.same_device:
+        args.dist_backend = "gloo"
+        args.launch_only = True
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))           # before anything touches a GPU
+    W = World(args)
+    try:
+        if args.dry_run:
+            run_dry(args, W)
+        elif args.workload == "br":
+            run_br(args, W)
+        elif args.workload == "br-host":
+            run_br_host(args, W)
+        else:
+            run_hf(args, W)
+    finally:
+        W.close()
 
 
 if __name__ == "__main__":

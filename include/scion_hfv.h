@@ -73,6 +73,10 @@ typedef struct hfv_ctx hfv_ctx;
 int hfv_ctx_create(int device, hfv_ctx **out);
 int hfv_ctx_destroy(hfv_ctx *ctx);
 int hfv_ctx_device(const hfv_ctx *ctx);
+/* NUMA node of the ctx's GPU (its PCIe root port), -1 if unknown.  The library's host worker
+ * threads (staging copies of the host-memory paths) run on that node's CPUs (HFV_NUMA_PIN=0:
+ * unpinned); a host feeder thread per GPU should be placed there too. */
+int hfv_ctx_numa_node(const hfv_ctx *ctx);
 void *hfv_ctx_stream(hfv_ctx *ctx);
 int hfv_ctx_set_keysel(hfv_ctx *ctx, int keysel);
 /* Offsets of the current InfoField / HopField inside each record (multiples of 8). */
@@ -168,6 +172,19 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms);
  * longer be written by other work when the call is made (synchronize their producers). */
 int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                        uint64_t *ticket);
+/* Post `count` batches in one call (tickets *first_ticket .. *first_ticket + count - 1), the
+ * many-descriptor form of hfv_service_submit (recvmmsg-style: one call per burst of RX
+ * batches).  All batches are checked before any is posted. */
+struct hfv_batch {
+    const void *recs;
+    size_t stride;
+    size_t n;
+    uint64_t *pass_bits;
+};
+int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket);
+/* Tickets are monotonic over the ctx's life, across service restarts (key changes, idle
+ * exits): a ticket of a stopped grid reports done, or -EIO if that grid exited on its idle
+ * timeout without verifying it. */
 /* 1 if the ticket's verdicts are complete in pass_bits (visible to any stream and to
  * copies), 0 if not yet. */
 int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket);
@@ -256,6 +273,11 @@ struct hfv_br_config {
 
 /* Install the router tables (copied; takes effect for batches enqueued afterwards). */
 int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
+/* The reference's ENABLE_HF_CHECK build switch (br/CMakeLists.txt:8,48-64) as a runtime
+ * setting: enable = 0 skips the hop-field MAC check (defer_verify_hop_field and the MAC block
+ * of border_router, path_processing.h:43-57 / xdp.c:259-274); default on.  Takes effect
+ * for batches enqueued afterwards; survives hfv_br_set_config. */
+int hfv_br_set_hf_check(hfv_ctx *ctx, int enable);
 /* Process n frames in place.  pkts: frame i at pkts + i*slot (slot % 8 == 0, >= 64);
  * len[i] its length (<= slot); ingress_ifindex[i] the receiving interface.  Outputs per
  * frame: action[i] = the XDP action returned (0 aborted, 1 drop, 2 pass, 4 redirect),

@@ -529,11 +529,14 @@ static int tx_port(const struct hfv_br_config *cfg, int ifindex)
     return 0;
 }
 
-static int border_router(pkt_t *k)
+/* border_router, xdp.c:250-283.  hf_check = 0 is the ENABLE_HF_CHECK=OFF build
+ * (br/CMakeLists.txt:8,48-64): defer_verify_hop_field and the MAC block compile to nothing
+ * (path_processing.h:43-57, xdp.c:259-274), everything else is unchanged. */
+static int border_router(pkt_t *k, int hf_check)
 {
     int v = process_packet(k);
     if (v > 0) return v;
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; hf_check && w < 2; ++w) {
         if (!(k->mask & (1u << w))) continue;
         if (!orc_verify_hop_field(k->macinput[w], k->mac[w], k->key)) return record(k, V_INVALID_HF);
     }
@@ -542,9 +545,9 @@ static int border_router(pkt_t *k)
     return record(k, verdict);
 }
 
-void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
-                    const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
-                    int32_t *egress_ifindex, uint64_t *stats)
+void orc_br_process_ex(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                       const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                       int32_t *egress_ifindex, uint64_t *stats, int hf_check)
 {
     for (size_t i = 0; i < n; ++i) {
         pkt_t k;
@@ -556,9 +559,16 @@ void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint3
         k.key = key0;
         k.stats = stats;
         k.last_verdict = 0;
-        int a = border_router(&k);
+        int a = border_router(&k, hf_check);
         action[i] = (uint8_t)a;
         verdict[i] = (uint8_t)k.last_verdict;
         egress_ifindex[i] = k.egress_ifindex;
     }
+}
+
+void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                    const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                    int32_t *egress_ifindex, uint64_t *stats)
+{
+    orc_br_process_ex(pkts, slot, len, ingress_ifindex, n, cfg, key0, action, verdict, egress_ifindex, stats, 1);
 }

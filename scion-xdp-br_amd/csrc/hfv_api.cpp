@@ -8,6 +8,8 @@
 // has completed (tracked with one event per table), so in-flight batches keep a stable
 // table.
 #include <errno.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -192,10 +194,16 @@ struct hfv_ctx {
     SvcShared *svc_host_dev = nullptr;
     SvcDesc *svc_mirror = nullptr;   // device copy of the descriptor ring (the grid's relay writes it)
     unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
-    uint64_t svc_next = 1;           // next ticket
+    uint64_t svc_next = 1;           // next grid-local batch number (1, 2, ... per grid)
+    uint64_t svc_base = 1;           // ticket of the running grid's batch 1 (tickets are monotonic per ctx)
+    uint64_t svc_ticket = 1;         // next ticket
+    std::vector<uint64_t> svc_lost;  // tickets of stopped grids that were never verified (bounded)
     uint64_t svc_tag = 0;            // generation of the running grid << 40 (see s_svc_tag)
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
 };
+
+static int device_numa(int device, cpu_set_t *cpus);
+static void note_numa(int device);
 
 // Any other data-path call on the ctx first stops a running service (after the batches
 // already posted): its grid holds every CU's LDS, so other kernels could not start until
@@ -321,6 +329,7 @@ int hfv_ctx_create(int device, hfv_ctx **out)
         return fail(rc, "hfv_ctx_create failed on device %d", device);
     }
     memset(c->shadow, 0, sizeof c->shadow);
+    note_numa(device);
     *out = c;
     return 0;
 }
@@ -368,6 +377,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
 }
 
 int hfv_ctx_device(const hfv_ctx *ctx) { return ctx ? ctx->device : -1; }
+int hfv_ctx_numa_node(const hfv_ctx *ctx) { return ctx ? device_numa(ctx->device, nullptr) : -1; }
 void *hfv_ctx_stream(hfv_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
 int hfv_ctx_set_keysel(hfv_ctx *ctx, int keysel)
@@ -449,8 +459,7 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
     const void *m = nullptr;
     int rc = keymap_open_ro(path, &m);
     if (rc == -ENOENT) {   // create an empty pinned map, as attachBr creates mac_key_map
-        rc = hfv_keymap_update(path, 0, &ctx->shadow[0]);
-        if (!rc) rc = hfv_keymap_erase(path, 0);
+        rc = keymap_create(path);   // header only: never touches a slot another process may write
         if (!rc) rc = keymap_open_ro(path, &m);
     }
     if (rc) return fail(rc, "cannot attach key map %s", path);
@@ -492,12 +501,12 @@ int hfv_key_add_batch(hfv_ctx *ctx, uint32_t first, const struct aes_key *keys, 
     if (!tmp) rc = -ENOMEM;
     if (!rc && hipMemcpyAsync(tmp, d_hk, sizeof(hop_key) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = -EIO;
     if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = -EIO;
-    if (!rc)
-        for (size_t i = 0; i < n; ++i) hfv_key_set_hop_key(ctx, first + (uint32_t)i, &tmp[i]);
+    if (rc) rc = fail(rc, "device key expansion failed");
+    for (size_t i = 0; !rc && i < n; ++i) rc = hfv_key_set_hop_key(ctx, first + (uint32_t)i, &tmp[i]);   // first error wins
     free(tmp);
     (void)hipFree(d_raw);
     (void)hipFree(d_hk);
-    return rc ? fail(rc, "device key expansion failed") : 0;
+    return rc;
 }
 
 // ---- data path ------------------------------------------------------------------------
@@ -665,7 +674,17 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
         cfg->n_egress > HFV_BR_MAX_IFACES || cfg->n_routes > HFV_BR_MAX_ROUTES || cfg->n_tx_ports > HFV_BR_MAX_TXPORTS)
         return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
                     HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
+    const uint32_t off = ctx->br.hf_check_off;
     compile_br_config(cfg, &ctx->br);
+    ctx->br.hf_check_off = off;
+    ctx->dirty = true;
+    return 0;
+}
+
+int hfv_br_set_hf_check(hfv_ctx *ctx, int enable)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    ctx->br.hf_check_off = enable ? 0u : 1u;
     ctx->dirty = true;
     return 0;
 }
@@ -751,6 +770,69 @@ static int host_threads()
     return t;
 }
 
+// NUMA placement of the host-side workers: the staging copies of a GPU's host path run on
+// the CPUs of the NUMA node its PCIe root port hangs off (one process per GPU, so the
+// first ctx of the process decides).  HFV_NUMA_PIN=0 leaves the threads unpinned.
+static std::mutex g_numa_m;
+static cpu_set_t g_numa_cpus;
+static bool g_numa_set = false;
+
+static void pin_to_numa()
+{
+    std::lock_guard<std::mutex> g(g_numa_m);
+    if (g_numa_set) (void)pthread_setaffinity_np(pthread_self(), sizeof g_numa_cpus, &g_numa_cpus);
+}
+
+// NUMA node of `device` (from its PCI bus id in sysfs) and that node's CPUs that this
+// process may run on; -1 if unknown.
+static int device_numa(int device, cpu_set_t *cpus)
+{
+    char bus[64] = {0}, path[256];
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return -1;
+    for (char *p = bus; *p; ++p)
+        if (*p >= 'A' && *p <= 'F') *p = (char)(*p - 'A' + 'a');
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    if (node < 0 || !cpus) return node;
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    f = fopen(path, "r");
+    if (!f) return node;
+    cpu_set_t allowed;
+    CPU_ZERO(cpus);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) CPU_ZERO(&allowed);
+    int a, b;
+    char sep;
+    while (fscanf(f, "%d", &a) == 1) {
+        b = a;
+        if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+            if (fscanf(f, "%d", &b) != 1) break;
+            if (fscanf(f, "%c", &sep) != 1) sep = 0;
+        }
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &allowed)) CPU_SET(c, cpus);
+        if (sep != ',') break;
+    }
+    fclose(f);
+    return node;
+}
+
+static void note_numa(int device)
+{
+    const char *e = getenv("HFV_NUMA_PIN");
+    if (e && atoi(e) == 0) return;
+    cpu_set_t cpus;
+    int node = device_numa(device, &cpus);
+    std::lock_guard<std::mutex> g(g_numa_m);
+    if (node >= 0 && !g_numa_set && CPU_COUNT(&cpus) > 0) {
+        g_numa_cpus = cpus;
+        g_numa_set = true;
+    }
+}
+
 // Persistent host worker threads for the staging copies (spawning threads per copy cost more
 // than the copies: 32 spawns per 2^20-frame router batch).  Part 0 of every job runs on the
 // calling thread, parts 1..nt-1 on the workers.  Jobs come from one ctx thread at a time.
@@ -758,7 +840,10 @@ class HostPool {
   public:
     explicit HostPool(int nt) : nt_(nt)
     {
-        for (int k = 1; k < nt_; ++k) th_.emplace_back([this, k] { work(k); });
+        for (int k = 1; k < nt_; ++k) th_.emplace_back([this, k] {
+            pin_to_numa();
+            work(k);
+        });
     }
     ~HostPool()
     {
@@ -1195,7 +1280,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
 
 }  // extern "C"
 
-// Ticket t is complete when every block of the grid has reported its share of it.
+// Grid-local batch t is complete when every block of the grid has reported its share of it.
 static bool svc_is_done(const hfv_ctx *ctx, uint64_t t)
 {
     const uint64_t *d = ctx->svc_host->done[(t - 1) % kSvcRing];
@@ -1217,19 +1302,21 @@ static int svc_wait_done(hfv_ctx *ctx, uint64_t t, int timeout_ms)
         if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0)
             return fail(-EIO, "verify service exited (%s); ticket %llu will not complete",
                         ctx->svc_host->status == kSvcIdleTimeout ? "idle timeout" : "watchdog",
-                        (unsigned long long)t);
+                        (unsigned long long)(ctx->svc_base + t - 1));
         if (hipStreamQuery(ctx->svc_stream) == hipSuccess)
-            return fail(-EIO, "verify service grid has exited; ticket %llu will not complete", (unsigned long long)t);
+            return fail(-EIO, "verify service grid has exited; ticket %llu will not complete",
+                        (unsigned long long)(ctx->svc_base + t - 1));
         clock_gettime(CLOCK_MONOTONIC, &now);
         double ms = (now.tv_sec - t0.tv_sec) * 1e3 + (now.tv_nsec - t0.tv_nsec) * 1e-6;
         if (timeout_ms >= 0 && ms > timeout_ms)
-            return fail(-ETIMEDOUT, "ticket %llu not done after %d ms", (unsigned long long)t, timeout_ms);
+            return fail(-ETIMEDOUT, "ticket %llu not done after %d ms", (unsigned long long)(ctx->svc_base + t - 1),
+                        timeout_ms);
     }
 }
 
 static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint64_t stride, uint64_t *ticket)
 {
-    const uint64_t t = ctx->svc_next;
+    const uint64_t t = ctx->svc_next;   // grid-local batch number
     if (t > kSvcRing) {   // the slot's previous batch must be done (and its descriptor read)
         int rc = svc_wait_done(ctx, t - kSvcRing, 60000);
         if (rc) return rc;
@@ -1241,7 +1328,10 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
     d->stride = stride;
     __atomic_store_n(&d->seq, ctx->svc_tag | t, __ATOMIC_RELEASE);
     ctx->svc_next = t + 1;
-    if (ticket) *ticket = t;
+    if (ticket) {   // a stop descriptor takes a grid slot but no ticket
+        *ticket = ctx->svc_base + t - 1;
+        ctx->svc_ticket = *ticket + 1;
+    }
     return 0;
 }
 
@@ -1265,11 +1355,31 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     // order; only the newest kSvcRing can still be open): scan those.  (The scan reads
     // kSvcRing x grid completion words, ~0.1 ms; it is not paid on a normal stop.)
     if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) return 0;
+    uint64_t first_lost = 0;
     for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t)
-        if (!svc_is_done(ctx, t))
-            return fail(-ETIMEDOUT, "verify service exited on its idle timeout before ticket %llu",
-                        (unsigned long long)t);
+        if (!svc_is_done(ctx, t)) {
+            first_lost = ctx->svc_base + t - 1;
+            if (ctx->svc_lost.size() >= 4096) ctx->svc_lost.erase(ctx->svc_lost.begin(), ctx->svc_lost.begin() + 1024);
+            ctx->svc_lost.push_back(first_lost);
+        }
+    if (first_lost)
+        return fail(-ETIMEDOUT, "verify service exited on its idle timeout before ticket %llu",
+                    (unsigned long long)first_lost);
     return 0;
+}
+
+// Ticket state: 1 done, 0 pending, -EIO lost (its grid stopped without verifying it),
+// -EINVAL never issued.  Tickets below the running grid's base belong to stopped grids,
+// which verified every batch posted to them unless they exited on a timeout (svc_lost).
+static int svc_ticket_state(const hfv_ctx *ctx, uint64_t ticket)
+{
+    if (!ctx->svc_host || ticket == 0 || ticket >= ctx->svc_ticket) return -EINVAL;
+    if (ticket < ctx->svc_base || !ctx->svc_running) {
+        for (uint64_t l : ctx->svc_lost)
+            if (l == ticket) return -EIO;
+        if (ticket < ctx->svc_base) return 1;
+    }
+    return svc_is_done(ctx, ticket - ctx->svc_base + 1) ? 1 : 0;
 }
 
 static int svc_quiesce(hfv_ctx *ctx) { return ctx->svc_running ? svc_stop(ctx, nullptr) : 0; }
@@ -1308,6 +1418,7 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     ctx->svc_hf_off = ctx->hf_off;
     ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
     ctx->svc_next = 1;
+    ctx->svc_base = ctx->svc_ticket;
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off, ctx->hf_off,
                                   (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream, ctx->svc_ev[0],
                                   ctx->svc_ev[1], &ctx->svc_grid);
@@ -1317,23 +1428,25 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     return 0;
 }
 
-int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
-                       uint64_t *ticket)
+static int svc_check_batch(const hfv_ctx *ctx, const void *recs, size_t stride, size_t n, const uint64_t *pass_bits)
 {
-    if (!ctx || !ticket) return fail(-EINVAL, "null argument");
-    *ticket = 0;
     if (n && (!recs || !pass_bits)) return fail(-EINVAL, "null buffer");
     if (n >= kSvcStopN / 2) return fail(-EINVAL, "batch too large");
     if (((uintptr_t)recs & 7) || (stride & 7) || ((uintptr_t)pass_bits & 7))
         return fail(-EINVAL, "records, stride and bitmap must be 8-byte aligned");
     if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
         return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
-    DeviceGuard g(ctx->device);
+    return 0;
+}
+
+// Restart the grid if it left on its idle timeout or if keys/keysel/layout changed (a batch
+// boundary), start it if it is not running.
+static int svc_ready(hfv_ctx *ctx)
+{
     if (ctx->svc_running && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0) {
-        // the grid left on its idle timeout (its posted batches were all done, or waits on
-        // them have reported -EIO): start a fresh one
-        (void)hipStreamSynchronize(ctx->svc_stream);
-        ctx->svc_running = false;
+        // the grid left on its idle timeout: reap it (batches it left unverified are recorded
+        // as lost for hfv_service_wait/poll) and start a fresh one
+        (void)svc_stop(ctx, nullptr);
     }
     // key, key-selection or layout changes take effect at this batch boundary; the grid's
     // batch counter is 32-bit, so the service also restarts every 2^31 batches
@@ -1347,21 +1460,66 @@ int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
         int rc = hfv_service_start(ctx, ctx->svc_idle_ms);
         if (rc) return rc;
     }
+    return 0;
+}
+
+int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
+                       uint64_t *ticket)
+{
+    if (!ctx || !ticket) return fail(-EINVAL, "null argument");
+    *ticket = 0;
+    int rc = svc_check_batch(ctx, recs, stride, n, pass_bits);
+    if (rc) return rc;
+    DeviceGuard g(ctx->device);
+    rc = svc_ready(ctx);
+    if (rc) return rc;
     return svc_post(ctx, (uint64_t)(uintptr_t)recs, (uint64_t)(uintptr_t)pass_bits, n, stride, ticket);
+}
+
+int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket)
+{
+    if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
+    *first_ticket = 0;
+    for (size_t i = 0; i < count; ++i) {
+        int rc = svc_check_batch(ctx, batches[i].recs, batches[i].stride, batches[i].n, batches[i].pass_bits);
+        if (rc) {
+            char why[256];
+            snprintf(why, sizeof why, "%s", hfv_last_error());
+            return fail(rc, "batch %zu: %s", i, why);
+        }
+    }
+    if (count == 0) return 0;
+    DeviceGuard g(ctx->device);
+    int rc = svc_ready(ctx);
+    if (rc) return rc;
+    for (size_t i = 0; i < count; ++i) {
+        uint64_t t = 0;
+        rc = svc_post(ctx, (uint64_t)(uintptr_t)batches[i].recs, (uint64_t)(uintptr_t)batches[i].pass_bits,
+                      batches[i].n, batches[i].stride, &t);
+        if (rc) return rc;   // batches 0..i-1 are posted (tickets *first_ticket ..)
+        if (i == 0) *first_ticket = t;
+    }
+    return 0;
 }
 
 int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)
 {
-    if (!ctx || !ctx->svc_host || ticket == 0 || ticket >= ctx->svc_next) return fail(-EINVAL, "unknown ticket");
-    return svc_is_done(ctx, ticket) ? 1 : 0;
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    int st = svc_ticket_state(ctx, ticket);
+    if (st == -EINVAL) return fail(-EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
+    if (st == -EIO) return fail(-EIO, "verify service stopped before ticket %llu", (unsigned long long)ticket);
+    return st;
 }
 
 int hfv_service_wait(hfv_ctx *ctx, uint64_t ticket, int timeout_ms)
 {
-    if (!ctx || !ctx->svc_host || ticket == 0 || ticket >= ctx->svc_next) return fail(-EINVAL, "unknown ticket");
-    if (svc_is_done(ctx, ticket)) return 0;
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    int st = svc_ticket_state(ctx, ticket);
+    if (st == -EINVAL) return fail(-EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
+    if (st == -EIO) return fail(-EIO, "verify service stopped before ticket %llu", (unsigned long long)ticket);
+    if (st == 1) return 0;
     if (!ctx->svc_running) return fail(-EIO, "verify service stopped before ticket %llu", (unsigned long long)ticket);
-    return svc_wait_done(ctx, ticket, timeout_ms);
+    return svc_wait_done(ctx, ticket - ctx->svc_base + 1, timeout_ms);
 }
 
 int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms)

@@ -613,7 +613,7 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
         // border_router, xdp.c:256-283: the deferred MAC check, then the redirect
         uint32_t v = A_ABORTED;
         bool ok = true;
-        if (k.need_mac) {
+        if (k.need_mac && !s_br.hf_check_off) {
             // slot-0 key (xdp.c:82) through the scalar cache, only where a hop field is checked
             const UniformKey ukey(keys);
             uint32_t t0, t1;

@@ -56,6 +56,7 @@ struct DevBrRoute {
 };
 struct DevBrConfig {
     uint32_t n_int, n_ing, n_egr, n_routes;
+    uint32_t hf_check_off, pad_[3];   // 1: the ENABLE_HF_CHECK=OFF router (hfv_br_set_hf_check)
     uint32_t tx_bits[HFV_BR_MAX_TXPORTS / 32];
     DevBrIntIface int_ifaces[HFV_BR_MAX_IFACES];
     DevBrIngress ingress[HFV_BR_MAX_IFACES];
@@ -159,6 +160,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);
+int keymap_create(const char *path);   // empty map (header only) if the file does not exist
 void keymap_close(const void *mapping);
 uint32_t keymap_seq(const void *mapping);
 uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8]);

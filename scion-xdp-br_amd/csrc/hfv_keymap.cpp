@@ -94,6 +94,17 @@ static inline uint32_t seq_load(const KeymapFile *km)
     return __atomic_load_n(&km->seq, __ATOMIC_ACQUIRE);
 }
 
+// Seqlock writer side (under the flock).  The odd store must be ordered before the slot
+// stores that follow it: a release store alone does not keep later stores behind it, so a
+// release fence follows it (a reader that saw the new slot bytes then also sees seq odd).
+// The even store is a release store: the slot stores are ordered before it.
+static inline void seq_begin(KeymapFile *km)
+{
+    __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELAXED);
+    std::atomic_thread_fence(std::memory_order_release);
+}
+static inline void seq_end(KeymapFile *km) { __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELEASE); }
+
 // Copy a consistent snapshot; returns the (even) seq it belongs to.
 uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8])
 {
@@ -125,6 +136,15 @@ void keymap_close(const void *mapping)
     if (mapping) munmap((void *)mapping, sizeof(KeymapFile));
 }
 
+int keymap_create(const char *path)
+{
+    KeymapFile *km;
+    int fd = map_file(path, true, true, &km);   // header written under the flock, slots untouched
+    if (fd < 0) return fd;
+    unmap_file(fd, km);
+    return 0;
+}
+
 }  // namespace hfv
 
 using namespace hfv;
@@ -148,10 +168,10 @@ int hfv_keymap_update(const char *path, uint32_t index, const struct hop_key *hk
     KeymapFile *km;
     int fd = map_file(path, true, true, &km);
     if (fd < 0) return fail(fd, "cannot open key map %s", path);
-    __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELEASE);   // odd: update in progress
+    seq_begin(km);   // odd: update in progress
     km->slot[index] = *hk;
     km->valid[index >> 5] |= 1u << (index & 31);
-    __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELEASE);   // even: published
+    seq_end(km);     // even: published
     unmap_file(fd, km);
     return 0;
 }
@@ -167,10 +187,10 @@ int hfv_keymap_erase(const char *path, uint32_t index)
     if (!((km->valid[index >> 5] >> (index & 31)) & 1u)) {
         rc = fail(-ENOENT, "key slot %u is empty", index);
     } else {
-        __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELEASE);
+        seq_begin(km);
         km->valid[index >> 5] &= ~(1u << (index & 31));
         memset(&km->slot[index], 0, sizeof(hop_key));
-        __atomic_store_n(&km->seq, km->seq + 1, __ATOMIC_RELEASE);
+        seq_end(km);
     }
     unmap_file(fd, km);
     return rc;

@@ -55,6 +55,7 @@ def lib():
         "hfv_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
         "hfv_ctx_destroy": (i32, [vp]),
         "hfv_ctx_device": (i32, [vp]),
+        "hfv_ctx_numa_node": (i32, [vp]),
         "hfv_ctx_stream": (vp, [vp]),
         "hfv_ctx_set_keysel": (i32, [vp, i32]),
         "hfv_ctx_set_record_layout": (i32, [vp, u32, u32]),
@@ -75,6 +76,7 @@ def lib():
         "hfv_keymap_read": (i32, [ctypes.c_char_p, vp, vp]),
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
+        "hfv_br_set_hf_check": (i32, [vp, i32]),
         "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_br_process_host": (i32, [vp, vp, sz, vp, vp, sz, sz, vp, vp, vp, vp]),
@@ -87,6 +89,7 @@ def lib():
         "hfv_verify_records_host": (i32, [vp, vp, sz, sz, vp]),
         "hfv_service_start": (i32, [vp, u32]),
         "hfv_service_submit": (i32, [vp, vp, sz, sz, vp, ctypes.POINTER(u64)]),
+        "hfv_service_submitv": (i32, [vp, vp, sz, ctypes.POINTER(u64)]),
         "hfv_service_poll": (i32, [vp, u64]),
         "hfv_service_wait": (i32, [vp, u64, i32]),
         "hfv_service_stop": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
@@ -194,6 +197,12 @@ def verify_macinput(macinput: bytes, expected: int, hop_key_bytes) -> bool:
 
 # ---- context --------------------------------------------------------------------------------
 
+class HfvBatch(ctypes.Structure):
+    """struct hfv_batch (hfv_service_submitv)"""
+    _fields_ = [("recs", ctypes.c_void_p), ("stride", ctypes.c_size_t), ("n", ctypes.c_size_t),
+                ("pass_bits", ctypes.c_void_p)]
+
+
 class Ctx:
     """One per GPU (hfv_ctx).  Mirrors the br-loader key commands and the XDP verify step."""
 
@@ -218,6 +227,27 @@ class Ctx:
             self.close()
         except Exception:
             pass
+
+    def numa_node(self):
+        """NUMA node of this GPU (-1 if unknown)."""
+        return lib().hfv_ctx_numa_node(self._h)
+
+    def numa_cpus(self):
+        """CPUs of this GPU's NUMA node that this process may run on (all allowed CPUs if the
+        node is unknown): where a per-GPU host feeder thread belongs."""
+        allowed = os.sched_getaffinity(0)
+        node = self.numa_node()
+        if node < 0:
+            return sorted(allowed)
+        try:
+            txt = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+        except OSError:
+            return sorted(allowed)
+        cpus = set()
+        for part in txt.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        return sorted(cpus & allowed) or sorted(allowed)
 
     @property
     def stream(self):
@@ -276,6 +306,10 @@ class Ctx:
     def br_set_config(self, cfg):
         _check(lib().hfv_br_set_config(self._h, ctypes.byref(cfg)))
 
+    def br_set_hf_check(self, enable: bool):
+        """ENABLE_HF_CHECK on/off (br/CMakeLists.txt:8): off skips the hop-field MAC check."""
+        _check(lib().hfv_br_set_hf_check(self._h, 1 if enable else 0))
+
     def br_process(self, pkts, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
                    stream=None):
         _check(lib().hfv_br_process(self._h, _ptr(pkts), slot, _ptr(lens), _ptr(ingress_ifindex), n, _ptr(action),
@@ -323,6 +357,18 @@ class Ctx:
         t = ctypes.c_uint64()
         _check(lib().hfv_service_submit(self._h, _ptr(recs), stride, n, _ptr(pass_bits), ctypes.byref(t)))
         return t.value
+
+    def service_submitv(self, batches):
+        """Post several batches in one call: batches = [(recs, n, pass_bits[, stride]), ...];
+        returns their tickets."""
+        arr = (HfvBatch * len(batches))()
+        for i, b in enumerate(batches):
+            recs, n, bits = b[0], b[1], b[2]
+            arr[i].recs, arr[i].n, arr[i].pass_bits = _ptr(recs), n, _ptr(bits)
+            arr[i].stride = b[3] if len(b) > 3 else REC_SIZE
+        t = ctypes.c_uint64()
+        _check(lib().hfv_service_submitv(self._h, arr, len(batches), ctypes.byref(t)))
+        return list(range(t.value, t.value + len(batches)))
 
     def service_poll(self, ticket):
         rc = lib().hfv_service_poll(self._h, ticket)

@@ -2,7 +2,9 @@
 """Workload for rocprofv3 --pmc passes: verify 2^20 and 2^24 records (config 2, and config 3
 with --keysel ifid), `reps` launches each, after one untimed generation pass.  With a 4th
 argument `svc` the batches go through the resident service instead: per size one 2-batch
-grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches."""
+grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches.  With a 5th
+argument `rotR` each size is held in R resident batches and batch k of a grid verifies
+batch k % R, exactly as bench.py's headline does (R x 64 MiB > the Infinity Cache)."""
 import os
 import sys
 
@@ -45,6 +47,7 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
     svc = len(sys.argv) > 4 and sys.argv[4] == "svc"
+    rot = int(sys.argv[5][3:]) if len(sys.argv) > 5 and sys.argv[5].startswith("rot") else 1
     torch.cuda.set_device(0)
     ctx = hfv.Ctx(0)
     if keysel == "ifid":
@@ -53,19 +56,20 @@ def main():
     else:
         ctx.key_add(0, KEY_1111)
     for n in sizes:
-        recs = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
-        bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
-        ctx.gen_records(recs, n, SEED_RECORDS)
+        R = rot if n <= (1 << 20) else 1
+        recs = [torch.empty((n, 64), dtype=torch.uint8, device="cuda") for _ in range(R)]
+        bits = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(max(R, reps))]
+        for i, r in enumerate(recs):   # consecutive generator dispatches = one size group (pmc_summary.py)
+            ctx.gen_records(r, n, SEED_RECORDS, first_index=i * n)
         if svc:
             torch.cuda.synchronize()
             for k in (2, reps):
                 ctx.service_start()
-                for _ in range(k):
-                    ctx.service_submit(recs, n, bits)
+                ctx.service_submitv([(recs[j % R], n, bits[j]) for j in range(k)])
                 ctx.service_stop()
         else:
-            for _ in range(reps):
-                ctx.verify_records(recs, n, bits)
+            for j in range(reps):
+                ctx.verify_records(recs[j % R], n, bits[j])
         torch.cuda.synchronize()
         del recs, bits
     ctx.close()

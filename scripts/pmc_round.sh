@@ -6,7 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 KS=${1:-zero}
 SVC=${2:-}          # "svc": batches through the resident service (10 per grid)
-OUT=gpurun_out/pmc_$KS${SVC:+_svc}
+ROT=${3:-rot1}      # "rot8": 8 resident 2^20 batches rotated, as in bench.py's headline
+OUT=gpurun_out/pmc_$KS${SVC:+_svc}_$ROT
 mkdir -p $OUT
 groups=(
   "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
@@ -22,7 +23,7 @@ for g in "${groups[@]}"; do
   i=$((i+1))
   echo "=== pass $i: $g"
   timeout -k 10 300 rocprofv3 --pmc $g --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
-      python3 scripts/pmc_driver.py $KS 10 1048576,16777216 $SVC > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
+      python3 scripts/pmc_driver.py $KS 10 1048576,16777216 ${SVC:-launch} $ROT > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
 if [[ $SVC == svc ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576,16777216 k_verify_service 10

@@ -23,12 +23,16 @@ def main(d, sizes, kernel="k_verify_records", per=1):
         group, first = -1, False
         if not kernel.startswith("k_verify"):   # one batch size: every launch of `kernel` but the first
             group, first = 0, True
+        prev_gen = False
         for did in sorted(disp):
             e = disp[did]
             if "k_gen_records" in e["name"]:
-                group += 1
+                if not prev_gen:   # consecutive generator dispatches fill one size's resident batches
+                    group += 1
+                prev_gen = True
                 first = True
                 continue
+            prev_gen = False
             if kernel not in e["name"] or group < 0:
                 continue
             if first:

@@ -21,13 +21,14 @@ class OracleBR:
 class GpuBR:
     """One BR instance backed by libscionhfv on the GPU (hfv_br_process)."""
 
-    def __init__(self, ctx, cfg, key0=KEYS[1]):
-        self.ctx, self.cfg, self.key0 = ctx, cfg, key0
+    def __init__(self, ctx, cfg, key0=KEYS[1], hf_check=True):
+        self.ctx, self.cfg, self.key0, self.hf_check = ctx, cfg, key0, hf_check
 
     def process(self, frames, lens, ifidx):
         import torch
         ctx = self.ctx
         ctx.br_set_config(self.cfg)
+        ctx.br_set_hf_check(self.hf_check)
         if self.key0 is None:
             try:
                 ctx.key_remove(0)

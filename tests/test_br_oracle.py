@@ -115,6 +115,28 @@ def test_bad_mac_and_missing_key():
     assert _run1(good, ifi, key0=T.KEYS[2])[:2] == (1, V["INVALID_HF"])
 
 
+def test_hf_check_off_forwards_bad_macs():
+    """ENABLE_HF_CHECK=OFF (br/CMakeLists.txt:8, path_processing.h:43, xdp.c:259-274): the same
+    frame with a corrupted hop-field MAC, or with no key installed, is forwarded and rewritten
+    exactly like the good frame with the check on."""
+    ing_enc, path, ifi = _direct()
+    good = ing_enc.frame(P.scion_header(path.pack()))
+    p = path.copy()
+    p.hops[1].mac = bytes([p.hops[1].mac[0] ^ 1]) + p.hops[1].mac[1:]
+    bad = ing_enc.frame(P.scion_header(p.pack()))
+    ref = _run1(good, ifi)
+    import orc
+    for frame, key0 in ((bad, T.KEYS[1]), (good, None)):
+        buf, lens = T.to_slots([frame])
+        hk = orc.hop_key(key0) if key0 is not None else None
+        a, v, e, s = orc.br_process(buf, lens, np.array([ifi], dtype=np.uint32), T.br_config("br1"), hk,
+                                    hf_check=False)
+        assert (int(a[0]), int(v[0]), int(e[0])) == ref[:3] == (4, V["SCION_FORWARD"], 3)
+        out = buf[0, :len(frame)].tobytes()
+        if frame is good:
+            assert out == ref[4]
+
+
 def test_unknown_egress_aborts_and_falls_through():
     """VERDICT_ABORT is XDP_ABORTED = 0, not > 0: the MAC check and the redirect still run and
     record a second verdict (xdp.c:194, 256-283)."""

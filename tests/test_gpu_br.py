@@ -30,11 +30,12 @@ def test_ptf_scenarios_gpu(gpu_ctx, v6):
         assert s[ifi, 0, 1] == len(frame) and s[ifi, 1, 1] == 1 and s.sum() == len(frame) + 1
 
 
-def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0):
+def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0, hf_check=True):
     ref = frames.copy()
-    oa, ov, oe, os_ = orc.br_process(ref, lens, ifidx, cfg, orc.hop_key(key0) if key0 is not None else None)
+    oa, ov, oe, os_ = orc.br_process(ref, lens, ifidx, cfg, orc.hop_key(key0) if key0 is not None else None,
+                                     hf_check=hf_check)
     got = frames.copy()
-    ga, gv, ge, gs = T.GpuBR(gpu_ctx, cfg, key0=key0).process(got, lens, ifidx)
+    ga, gv, ge, gs = T.GpuBR(gpu_ctx, cfg, key0=key0, hf_check=hf_check).process(got, lens, ifidx)
     bad = np.nonzero((ga != oa) | (gv != ov) | (ge != oe) | (got != ref).any(axis=1))[0]
     assert bad.size == 0, "first mismatch at frame %d: gpu (%d,%d,%d) oracle (%d,%d,%d)" % (
         bad[0], ga[bad[0]], gv[bad[0]], ge[bad[0]], oa[bad[0]], ov[bad[0]], oe[bad[0]])
@@ -63,6 +64,19 @@ def test_fuzz_parity_no_key_and_foreign_key(gpu_ctx):
     fwd = np.nonzero(v == hfv.VERDICT["SCION_FORWARD"])[0]
     assert np.isin(ifidx[fwd], [5, 7]).all()          # BR 1's internal interfaces
     _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[5])
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+def test_fuzz_parity_hf_check_off(gpu_ctx, v6):
+    """ENABLE_HF_CHECK=OFF (br/CMakeLists.txt:8): no frame is dropped for its hop-field MAC,
+    everything else as with the check; bit-exact against the oracle built the same way."""
+    brs = {b: T.OracleBR(T.br_config(b, v6)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, v6, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", v6, 20000, seed=200 + v6, payload_max=1500)
+    v = _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", v6), T.KEYS[1], hf_check=False)
+    assert hfv.VERDICT["INVALID_HF"] not in v
+    _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", v6), None, hf_check=False)   # no key: still forwarded
+    gpu_ctx.br_set_hf_check(True)
 
 
 def test_large_batch_mixed_sizes(gpu_ctx):

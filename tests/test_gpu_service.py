@@ -154,6 +154,51 @@ def test_service_key_change_is_a_batch_boundary(ctx):
     assert np.array_equal(bits_np(outs[2], n), g["pass_bits"])
 
 
+def test_service_tickets_monotonic_across_restarts(ctx):
+    """three batches, a key change (grid restart at the batch boundary), three
+    more, then an explicit restart through the launch path: every ticket is distinct and
+    waiting on any earlier one reports it done (not 'unknown', not an alias of a new batch)."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    outs = [new_bits(n, fill=-1) for _ in range(7)]
+    torch.cuda.synchronize()
+    ts = [ctx.service_submit(d, n, outs[i]) for i in range(3)]
+    ctx.key_add(1, orc.KEY_1111)                   # key table changed: restart at the next submit
+    ts += ctx.service_submitv([(d, n, outs[i]) for i in range(3, 6)])
+    ctx.verify_records(d, n, outs[6])              # launch path: stops the service
+    ts.append(ctx.service_submit(d, n, new_bits(n)))
+    assert len(set(ts)) == len(ts) and ts == sorted(ts)
+    for t in ts:
+        ctx.service_wait(t, 20000)
+        assert ctx.service_poll(t)
+    for o in outs:
+        assert np.array_equal(bits_np(o, n), g["pass_bits"])
+    with pytest.raises(hfv.HfvError):
+        ctx.service_wait(ts[-1] + 1)               # never issued
+
+
+def test_service_submitv_golden_ifid(ctx):
+    """Several batches posted by one hfv_service_submitv call, 256-key table (config 3)."""
+    g = orc.load_golden("hf_ifid256.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    nk = int(g["nkeys"])
+    raw = g["raw_keys"].reshape(-1).tobytes()[:16 * nk]
+    ctx.key_add_batch(0, raw)
+    ctx.set_keysel(hfv.KEYSEL_IFID)
+    parts = [(0, 1), (1, 333), (333, 640), (640, n)]
+    outs = [new_bits(b - a, fill=-1) for a, b in parts]
+    torch.cuda.synchronize()
+    ts = ctx.service_submitv([(d[a:], b - a, o) for (a, b), o in zip(parts, outs)])
+    for t in ts:
+        ctx.service_wait(t, 20000)
+    hk, valid = orc.key_table(raw)
+    for (a, b), o in zip(parts, outs):
+        assert np.array_equal(bits_np(o, b - a), orc.verify_records(g["records"][a:b], hk, valid, 1))
+
+
 def test_service_no_key_fails_closed(ctx):
     g = orc.load_golden("hf_single.npz")
     n = len(g["records"])

@@ -1,0 +1,47 @@
+"""bench.py's multi-GPU launcher: `--gpus N` without a torch.distributed
+environment starts N rank processes itself, before anything touches a GPU, and the JSON line
+reports the initialised world.  CPU: --dry-run (gloo ranks, no GPU work).  GPU: two product
+ranks sharing GPU 0 through the launch path (one MI355X per box; the service grid needs the
+whole GPU, so ranks that share one run the launch path)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=300):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_dry_run_launches_n_ranks(n):
+    d = _bench("--dry-run", "--gpus", str(n), "--n", "100", "--steps", "3", "--warmup", "1")
+    assert d["n_gpus"] == n
+    assert len(d["per_rank_ms"]) == n
+    assert d["backend"] == "gloo"
+
+
+def test_dry_run_single_rank_does_not_spawn():
+    d = _bench("--dry-run", "--steps", "2")
+    assert d["n_gpus"] == 1 and len(d["per_rank_ms"]) == 1
+
+
+@pytest.mark.gpu
+def test_two_product_ranks_on_one_gpu():
+    """Two ranks, each verifying its own resident records with the HIP kernels (launch path),
+    every bitmap checked against the generator truth inside bench.py."""
+    d = _bench("--gpus", "2", "--same-device", "--n", "65536", "--rotate", "2", "--steps", "4", "--warmup", "2",
+               "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
+    assert d["n_gpus"] == 2
+    assert len(d["per_rank_ms"]["all"]) == 2
+    assert d["value"] > 0 and d["roofline"]["kernel"] == "k_verify_records"

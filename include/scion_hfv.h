@@ -109,6 +109,8 @@ int hfv_key_get(hfv_ctx *ctx, uint32_t index, struct hop_key *out);
 int hfv_keymap_path(const char *br, char *out, size_t len);
 /* Map::update of one slot, creating the map file if needed. */
 int hfv_keymap_update(const char *path, uint32_t index, const struct hop_key *hk);
+/* An empty map (no slot written) if the file does not exist yet; an existing map is kept. */
+int hfv_keymap_create(const char *path);
 /* Map::erase of one slot; -ENOENT if it was empty. */
 int hfv_keymap_erase(const char *path, uint32_t index);
 /* Consistent snapshot of all HFV_MAX_KEYS slots and the 256-bit valid mask. */
@@ -278,6 +280,45 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
  * of border_router, path_processing.h:43-57 / xdp.c:259-274); default on.  Takes effect
  * for batches enqueued afterwards; survives hfv_br_set_config. */
 int hfv_br_set_hf_check(hfv_ctx *ctx, int enable);
+/* ---- control plane: br-loader's configuration path ---------------------------------------
+ * loadConfig + initializeMaps (br/src/config.cpp:212-262, maps.cpp:91-200, called by attachBr,
+ * br_loader.cpp:88-151) for C hosts: the br-loader TOML file (`self`, `topology`,
+ * `internal_interfaces`, br/README.md) and the SCION topology.json it names are parsed, each
+ * local underlay address is resolved to the interface holding it, and the router tables are
+ * built.  The next-hop table replaces bpf_fib_lookup (no kernel FIB on the GPU). */
+struct hfv_br_ifaddr {             /* one address of the getifaddrs view (config.cpp:168-204) */
+    char ifname[16];
+    uint32_t ifindex;
+    uint32_t family;               /* HFV_AF_INET / HFV_AF_INET6 */
+    uint8_t addr[16];
+};
+struct hfv_br_next_hop {           /* one static FIB entry */
+    uint32_t family;
+    uint8_t prefix[16];
+    uint32_t prefix_len;
+    char ifname[16];
+    uint8_t smac[6];
+    uint8_t dmac[6];
+    int32_t ret;                   /* BPF_FIB_LKUP_RET_*, 0 = forward */
+};
+/* ifaddrs NULL: this network namespace (getifaddrs + if_nametoindex).  self, listing and diag
+ * (each nullable, NUL-terminated, truncated to their length) receive the BR name, the
+ * "XDP Border Router ..." listing br-loader prints and br-loader's stderr messages (the error,
+ * or the "WARNING: No interface has IP ..." lines).  Returns 0, -EINVAL for a configuration
+ * br-loader rejects, -ENOSPC if the tables exceed the fixed capacity. */
+int hfv_br_config_load(const char *toml_path, const struct hfv_br_ifaddr *ifaddrs, size_t n_ifaddrs,
+                       const struct hfv_br_next_hop *hops, size_t n_hops, struct hfv_br_config *out,
+                       char *self, size_t self_len, char *listing, size_t listing_len, char *diag, size_t diag_len);
+/* The same with this namespace's interfaces, installed into ctx (hfv_br_set_config). */
+int hfv_br_load_config(hfv_ctx *ctx, const char *toml_path, const struct hfv_br_next_hop *hops, size_t n_hops);
+/* Pinned router tables, $HFV_PIN_DIR/<br>/br_config: `hfv-loader attach` publishes them (the
+ * maps attachBr fills and pins), a data plane attached with hfv_ctx_attach_brconfig reloads
+ * them whenever they are republished, at the next batch boundary.  Writers flock; readers see
+ * whole tables (seqlock). */
+int hfv_brconfig_path(const char *br, char *out, size_t len);
+int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg);
+int hfv_brconfig_read(const char *path, struct hfv_br_config *cfg);
+int hfv_ctx_attach_brconfig(hfv_ctx *ctx, const char *path);
 /* Process n frames in place.  pkts: frame i at pkts + i*slot (slot % 8 == 0, >= 64);
  * len[i] its length (<= slot); ingress_ifindex[i] the receiving interface.  Outputs per
  * frame: action[i] = the XDP action returned (0 aborted, 1 drop, 2 pass, 4 redirect),

@@ -164,6 +164,9 @@ struct hfv_ctx {
     const void *keymap = nullptr;
     uint32_t keymap_seq = 0xffffffffu;
     char keymap_path[4096] = {0};
+    // attached pinned router tables (hfv_ctx_attach_brconfig)
+    const void *brmap = nullptr;
+    uint32_t brmap_seq = 0xffffffffu;
     // dispatch timing (hfv_verify_records_timed)
     hipEvent_t tev[2] = {nullptr, nullptr};
     // router tables for hfv_br_process (published with the key table)
@@ -230,6 +233,17 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         uint32_t seq = keymap_seq(ctx->keymap);
         if (seq != ctx->keymap_seq) {
             ctx->keymap_seq = keymap_snapshot(ctx->keymap, ctx->shadow, ctx->valid);
+            ctx->dirty = true;
+        }
+    }
+    if (ctx->brmap) {    // router tables republished by `hfv-loader attach`
+        uint32_t seq = brcfg_seq(ctx->brmap);
+        if (seq != ctx->brmap_seq) {
+            hfv_br_config cfg;
+            ctx->brmap_seq = brcfg_snapshot(ctx->brmap, &cfg);
+            const uint32_t off = ctx->br.hf_check_off;
+            compile_br_config(&cfg, &ctx->br);
+            ctx->br.hf_check_off = off;
             ctx->dirty = true;
         }
     }
@@ -366,6 +380,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
     if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
     if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
     keymap_close(ctx->keymap);
+    brcfg_close(ctx->brmap);
     for (int i = 0; i < 2; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
@@ -678,6 +693,27 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
     compile_br_config(cfg, &ctx->br);
     ctx->br.hf_check_off = off;
     ctx->dirty = true;
+    return 0;
+}
+
+int hfv_br_load_config(hfv_ctx *ctx, const char *toml_path, const struct hfv_br_next_hop *hops, size_t n_hops)
+{
+    if (!ctx || !toml_path) return fail(-EINVAL, "null argument");
+    hfv_br_config cfg;
+    int rc = hfv_br_config_load(toml_path, nullptr, 0, hops, n_hops, &cfg, nullptr, 0, nullptr, 0, nullptr, 0);
+    if (rc) return rc;
+    return hfv_br_set_config(ctx, &cfg);
+}
+
+int hfv_ctx_attach_brconfig(hfv_ctx *ctx, const char *path)
+{
+    if (!ctx || !path) return fail(-EINVAL, "null argument");
+    const void *m = nullptr;
+    int rc = brcfg_open_ro(path, &m);
+    if (rc) return fail(rc, "cannot attach pinned router config %s", path);
+    brcfg_close(ctx->brmap);
+    ctx->brmap = m;
+    ctx->brmap_seq = 0xffffffffu;   // loaded at the next batch boundary
     return 0;
 }
 
@@ -1391,11 +1427,11 @@ static bool svc_keys_changed(hfv_ctx *ctx)
 
 extern "C" {
 
-int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
+// A new service grid in two halves, so that a submit can post its batches into the ring
+// between them and the grid finds them there when it starts: svc_begin (generation tag, key
+// table, bookkeeping) and svc_launch.
+static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
 {
-    if (!ctx) return fail(-EINVAL, "ctx is NULL");
-    if (ctx->svc_running) return 0;
-    DeviceGuard g(ctx->device);
     if (!ctx->svc_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&ctx->svc_stream, hipStreamNonBlocking));
         HIP_TRY(hipHostMalloc((void **)&ctx->svc_host, sizeof(SvcShared),
@@ -1410,8 +1446,7 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     // table carry a smaller tag and never match
     ctx->svc_tag += 1ull << 40;
     __atomic_store_n(&ctx->svc_host->status, 0, __ATOMIC_RELEASE);
-    DevState *ds;
-    int rc = publish_keys(ctx, ctx->svc_stream, &ds);
+    int rc = publish_keys(ctx, ctx->svc_stream, ds);
     if (rc) return rc;
     ctx->svc_keysel = ctx->keysel;
     ctx->svc_inf_off = ctx->inf_off;
@@ -1419,13 +1454,29 @@ int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
     ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
     ctx->svc_next = 1;
     ctx->svc_base = ctx->svc_ticket;
-    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off, ctx->hf_off,
-                                  (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream, ctx->svc_ev[0],
-                                  ctx->svc_ev[1], &ctx->svc_grid);
-    rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
+    return 0;
+}
+
+static int svc_launch(hfv_ctx *ctx, DevState *ds)
+{
+    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
+                                  ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream,
+                                  ctx->svc_ev[0], ctx->svc_ev[1], &ctx->svc_grid);
+    int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ctx->svc_running = true;
     return 0;
+}
+
+int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (ctx->svc_running) return 0;
+    DeviceGuard g(ctx->device);
+    DevState *ds;
+    int rc = svc_begin(ctx, idle_ms, &ds);
+    if (rc) return rc;
+    return svc_launch(ctx, ds);
 }
 
 static int svc_check_batch(const hfv_ctx *ctx, const void *recs, size_t stride, size_t n, const uint64_t *pass_bits)
@@ -1440,9 +1491,11 @@ static int svc_check_batch(const hfv_ctx *ctx, const void *recs, size_t stride, 
 }
 
 // Restart the grid if it left on its idle timeout or if keys/keysel/layout changed (a batch
-// boundary), start it if it is not running.
-static int svc_ready(hfv_ctx *ctx)
+// boundary); if no grid runs, begin one and return its table in *launch (the caller posts its
+// batches, then launches it with svc_launch), else *launch = nullptr.
+static int svc_ready(hfv_ctx *ctx, DevState **launch)
 {
+    *launch = nullptr;
     if (ctx->svc_running && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0) {
         // the grid left on its idle timeout: reap it (batches it left unverified are recorded
         // as lost for hfv_service_wait/poll) and start a fresh one
@@ -1456,10 +1509,7 @@ static int svc_ready(hfv_ctx *ctx)
         int rc = svc_stop(ctx, nullptr);
         if (rc) return rc;
     }
-    if (!ctx->svc_running) {
-        int rc = hfv_service_start(ctx, ctx->svc_idle_ms);
-        if (rc) return rc;
-    }
+    if (!ctx->svc_running) return svc_begin(ctx, ctx->svc_idle_ms, launch);
     return 0;
 }
 
@@ -1468,12 +1518,8 @@ int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
 {
     if (!ctx || !ticket) return fail(-EINVAL, "null argument");
     *ticket = 0;
-    int rc = svc_check_batch(ctx, recs, stride, n, pass_bits);
-    if (rc) return rc;
-    DeviceGuard g(ctx->device);
-    rc = svc_ready(ctx);
-    if (rc) return rc;
-    return svc_post(ctx, (uint64_t)(uintptr_t)recs, (uint64_t)(uintptr_t)pass_bits, n, stride, ticket);
+    struct hfv_batch b = {recs, stride, n, pass_bits};
+    return hfv_service_submitv(ctx, &b, 1, ticket);
 }
 
 int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket)
@@ -1483,6 +1529,7 @@ int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t co
     for (size_t i = 0; i < count; ++i) {
         int rc = svc_check_batch(ctx, batches[i].recs, batches[i].stride, batches[i].n, batches[i].pass_bits);
         if (rc) {
+            if (count == 1) return rc;
             char why[256];
             snprintf(why, sizeof why, "%s", hfv_last_error());
             return fail(rc, "batch %zu: %s", i, why);
@@ -1490,16 +1537,24 @@ int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t co
     }
     if (count == 0) return 0;
     DeviceGuard g(ctx->device);
-    int rc = svc_ready(ctx);
+    DevState *launch = nullptr;
+    int rc = svc_ready(ctx, &launch);
     if (rc) return rc;
     for (size_t i = 0; i < count; ++i) {
+        // a new grid is launched once the ring holds the first batches (at most a ring's
+        // worth: posting more waits for completions), so it finds them when it starts
+        if (launch && i == (size_t)kSvcRing) {
+            rc = svc_launch(ctx, launch);
+            launch = nullptr;
+            if (rc) return rc;
+        }
         uint64_t t = 0;
         rc = svc_post(ctx, (uint64_t)(uintptr_t)batches[i].recs, (uint64_t)(uintptr_t)batches[i].pass_bits,
                       batches[i].n, batches[i].stride, &t);
         if (rc) return rc;   // batches 0..i-1 are posted (tickets *first_ticket ..)
         if (i == 0) *first_ticket = t;
     }
-    return 0;
+    return launch ? svc_launch(ctx, launch) : 0;
 }
 
 int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)
@@ -1533,12 +1588,24 @@ int hfv_service_running(const hfv_ctx *ctx) { return ctx && ctx->svc_running ? 1
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
 // 0 loaded ring slot i's descriptor (i < kSvcRing); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and
-// s_memrealtime at its start and at its exit (the shader clock over the grid's life).
+// s_memrealtime at its start and at its exit (the shader clock over the grid's life);
+// out[kSvcRing + 4 + i] = s_memrealtime when the relay published slot i (2 * kSvcRing + 4 words).
 int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
 {
     if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
     for (uint32_t i = 0; i < kSvcRing; ++i) out[i] = __atomic_load_n(&ctx->svc_host->load_clock[i], __ATOMIC_ACQUIRE);
     for (uint32_t i = 0; i < 4; ++i) out[kSvcRing + i] = __atomic_load_n(&ctx->svc_host->run_clock[i], __ATOMIC_ACQUIRE);
+    for (uint32_t i = 0; i < kSvcRing; ++i)
+        out[kSvcRing + 4 + i] = __atomic_load_n(&ctx->svc_host->relay_clock[i], __ATOMIC_ACQUIRE);
+    return 0;
+}
+
+// Diagnostic: the HFV_SVC_PROF phase counters (SvcShared::prof) summed over all grids since
+// the last call, then cleared.
+extern "C" int hfv_debug_service_prof(hfv_ctx *ctx, uint64_t *out8)
+{
+    if (!ctx || !out8 || !ctx->svc_host) return fail(-EINVAL, "bad argument");
+    for (int i = 0; i < 8; ++i) out8[i] = __atomic_exchange_n(&ctx->svc_host->prof[i], 0, __ATOMIC_ACQ_REL);
     return 0;
 }
 

@@ -98,6 +98,8 @@ struct SvcShared {
     uint64_t pad[7];
     uint64_t load_clock[kSvcRing];   // diagnostics: s_memrealtime when block 0 loaded the slot
     uint64_t run_clock[4];           // diagnostics: block 0 wave 0 s_memtime/s_memrealtime at start, at exit
+    uint64_t relay_clock[kSvcRing];  // diagnostics: s_memrealtime when the relay published the slot
+    uint64_t prof[8];                // diagnostics (HFV_SVC_PROF builds): shader cycles per loop phase, summed over waves
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
@@ -161,6 +163,11 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);
 int keymap_create(const char *path);   // empty map (header only) if the file does not exist
+// pinned router tables (hfv_config.cpp)
+int brcfg_open_ro(const char *path, const void **mapping);
+void brcfg_close(const void *mapping);
+uint32_t brcfg_seq(const void *mapping);
+uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out);
 void keymap_close(const void *mapping);
 uint32_t keymap_seq(const void *mapping);
 uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8]);

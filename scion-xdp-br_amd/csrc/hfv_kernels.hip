@@ -650,6 +650,27 @@ struct SvcTile {   // one claimed tile, wave-uniform
 };
 enum SvcClaim { kSvcFound = 0, kSvcStop = 1, kSvcPending = 2 };
 
+// One tile's words for the resident service: the tile's base address is wave-uniform (one
+// SGPR pair) and each lane adds a 32-bit offset (global_load ... saddr form); lanes past the
+// batch's last record re-read it.
+__device__ __forceinline__ RecWords load_tile(const SvcTile &t, uint32_t lane, uint32_t inf_off, uint32_t hf_off)
+{
+    const uint64_t first = t.tile * 64;
+    const uint64_t left = t.n - 1 - first;                       // uniform: last valid lane
+    const uint32_t lim = left < 63 ? (uint32_t)left : 63u;
+    const uint32_t off = (lane < lim ? lane : lim) * (uint32_t)t.stride;
+    const GlobalU8 *p = (const GlobalU8 *)(t.recs + first * t.stride) + off;
+    typedef const __attribute__((address_space(1))) u32x2 *P2;
+    typedef const __attribute__((address_space(1))) uint32_t *P1;
+    const u32x2 a = *reinterpret_cast<P2>(p + inf_off);
+    const u32x2 b = *reinterpret_cast<P2>(p + hf_off);
+    RecWords r;
+    r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
+    r.inf = make_uint2(a.x, a.y);
+    r.hfa = make_uint2(b.x, b.y);
+    return r;
+}
+
 __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 {
     return (uint64_t)wave_uniform((uint32_t)x) | ((uint64_t)wave_uniform((uint32_t)(x >> 32)) << 32);
@@ -658,6 +679,47 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 #ifndef HFV_SVC_ACQ
 #define HFV_SVC_ACQ 1   // 0: none, 1: acquire fence per loaded batch, 2: system-scope record loads
 #endif
+// HFV_SVC_PROF = 1: diagnostic build; every wave sums the shader cycles (s_memtime) it spends
+// in each phase of the service loop and adds them to host->prof[] at exit:
+//   0 waiting for the current tile's records at the top of the loop, 1 claim + map + next
+//   tile's loads, 2 the tile's AES rounds and verdict, 3 verdict stores + completion count,
+//   4 blocking waits for a descriptor, 5 tiles verified, 6 the wave's whole loop.
+#ifndef HFV_SVC_PROF
+#define HFV_SVC_PROF 0
+#endif
+// Only wave 1 of every block samples (s_memtime from every wave of a CU slowed the loop
+// many times over); the other waves run the plain loop beside it.
+struct SvcProf {
+    uint64_t c[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t t = 0;
+    bool on = false;
+    __device__ __forceinline__ void start()
+    {
+        if constexpr (HFV_SVC_PROF) {
+            on = wave_uniform(threadIdx.x >> 6) == 1;
+            if (on) t = __builtin_amdgcn_s_memtime();
+        }
+    }
+    __device__ __forceinline__ void mark(int k)
+    {
+        if constexpr (HFV_SVC_PROF) {
+            if (!on) return;
+            uint64_t now = __builtin_amdgcn_s_memtime();
+            c[k] += now - t;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void flush(SvcShared *host, uint32_t lane, uint64_t t0)
+    {
+        if constexpr (HFV_SVC_PROF) {
+            if (!on) return;
+            c[6] = __builtin_amdgcn_s_memtime() - t0;
+            if (lane == 0)
+                for (int k = 0; k < 7; ++k)
+                    __hip_atomic_fetch_add(&host->prof[k], c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+};
 
 // This block's share of batch b is verified (one lane).  The verdict words were written
 // through to memory (system-scope stores) and every wave waited for its stores'
@@ -716,6 +778,8 @@ __device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks)
         __hip_atomic_store(&m->stride, stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&m->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&host->relay_clock[slot], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);   // diagnostics (a posted write)
         if (n == kSvcStopN) return;
     }
 }
@@ -744,8 +808,11 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // fields only after seq was seen
 #if HFV_SVC_ACQ == 1
-    // the batch's records were written before the host posted it: drop stale cache lines
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // the batch's records were written (by a kernel or a copy into device memory) before the
+    // host posted it: drop this CU's stale L1 lines (agent scope, buffer_inv sc1)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#elif HFV_SVC_ACQ == 3
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope (buffer_inv sc0 sc1: L1 and L2)
 #endif
     if (blockIdx.x == 0)
         __hip_atomic_store(&host->load_clock[slot], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
@@ -909,75 +976,123 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
     uint32_t mb = 0;
-    SvcTile cur, none;
+    SvcTile none;
     none.base = 0;
     none.count = 0;
-    uint32_t g = 0;
-    if (lane == 0) g = __hip_atomic_fetch_add(&s_svc_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (svc_map(host, mir, idle_ticks, lane, wave_uniform(g), true, mb, none, cur) != kSvcFound) return;
-    uint32_t pending = 0;   // verified tiles of cur.b not counted yet
-    // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
-    // out as ONE scattered write-through store when the wave leaves the batch or the stash
-    // is full.  A store per tile would sit in the wave's in-order vmcnt queue in front of
-    // the next tile's record loads and expose its (memory-side) acknowledge every tile.
-    // (Collecting a block's words in LDS and writing 512 B chunks instead was not faster.)
-    uint64_t st_word = 0, st_tile = 0;
-    uint32_t stashed = 0;
-    auto load = [&](const SvcTile &t) {
-        if constexpr (HFV_SVC_ACQ == 2)
-            return load_rec_sys((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
-        else
-            return load_rec<false>((const uint8_t *)t.recs, t.stride, t.tile * 64 + lane, t.n - 1, inf_off, hf_off);
-    };
-    RecWords rc = load(cur);
-    svc_prefetch(host, mir, idle_ticks, lane, cur.b);
-    for (;;) {
-        // This tile's record words are complete before the next tile's loads are issued:
-        // without this explicit wait (a builtin, so the waitcnt pass sees it) the pass merges
-        // the loop's several entry paths and puts a vmcnt(0) AFTER the next tile's loads, in
-        // front of this tile's rounds, which serialises load latency and compute per tile.
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
-        // claim and prefetch the next tile before computing this one; a claim in a batch
-        // the host has not posted yet is resolved after this tile is counted, so a host
-        // that waits for this batch before posting the next never waits on us
-        g = 0;
+    // The loop, per tile: wait for the tile's records (loaded one iteration ahead), take the
+    // tile number claimed one iteration ago and claim the next (LDS atomic; its latency hides
+    // behind the rounds), store the verdict words of a batch the wave left in the previous
+    // iteration (so their write acknowledgement arrives while this tile computes and is
+    // covered by the next iteration's wait), map the next tile and issue its loads, compute.
+    // Measured with the HFV_SVC_PROF build on the loop this replaces (claim at the top, store
+    // and a vmcnt(0) drain when leaving a batch): claim/map/load 10 %, store/count drain
+    // 9-20 % of a wave's cycles.
+    auto claim = [&]() -> uint32_t {
+        uint32_t g = 0;
         if (lane == 0) g = __hip_atomic_fetch_add(&s_svc_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        g = wave_uniform(g);
+        return g;
+    };
+    SvcTile cur;
+    if (svc_map(host, mir, idle_ticks, lane, wave_uniform(claim()), true, mb, none, cur) != kSvcFound) return;
+    uint32_t gq = claim();   // the next tile's number (lane 0), read one iteration later
+    // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
+    // out as ONE scattered write-through store, issued at the top of the iteration after the
+    // wave left the batch (or filled the stash).  A store per tile would sit in the wave's
+    // in-order vmcnt queue in front of the next tile's record loads.  (Collecting a block's
+    // words in LDS and writing 512 B chunks instead was not faster.)
+    uint64_t st_word = 0, st_tile = 0, st_bits = 0;
+    uint32_t stashed = 0;
+    bool flush = false;              // the stash holds words to store at the next top
+    uint32_t fl_b = 0, fl_count = 0, fl_k = 0;   // ... and the count they complete (fl_k = 0: none)
+    uint32_t dc_b = 0, dc_count = 0, dc_k = 0;   // stored last iteration: count after this wait
+    uint32_t pending = 0;            // verified tiles of cur.b not handed to a count yet
+    auto count = [&](uint32_t b, uint32_t cnt, uint32_t k) {   // stores acknowledged (caller waited)
+        if (k && lane == 0) {
+            const uint32_t old =
+                __hip_atomic_fetch_add(&s_svc[b % kSvcRing].done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old + k == cnt) svc_complete(host, b);
+        }
+    };
+    auto store_stash = [&]() {
+        if (lane < stashed)
+            __hip_atomic_store(reinterpret_cast<GlobalU64 *>(st_bits) + st_tile, st_word, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        stashed = 0;
+    };
+    RecWords rc = load_tile(cur, lane, inf_off, hf_off);
+    svc_prefetch(host, mir, idle_ticks, lane, cur.b);
+    SvcProf prof;
+    const uint64_t prof_t0 = HFV_SVC_PROF ? __builtin_amdgcn_s_memtime() : 0;
+    prof.start();
+    for (;;) {
+        // This tile's record words (and every earlier store) are complete.  An explicit wait
+        // (a builtin, so the waitcnt pass sees it): without it the pass merges the loop's
+        // entry paths and puts a vmcnt(0) AFTER the next tile's loads.
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+        count(dc_b, dc_count, dc_k);           // the stores of the previous iteration are acknowledged
+        dc_k = 0;
+        prof.mark(0);
+        if (flush) {                           // the batch left in the previous iteration
+            store_stash();
+            dc_b = fl_b;
+            dc_count = fl_count;
+            dc_k = fl_k;
+            flush = false;
+        }
+        const uint32_t g = wave_uniform(gq);
+        gq = claim();
         SvcTile nx;
         SvcClaim c = svc_map(host, mir, idle_ticks, lane, g, false, mb, cur, nx);
         if (c != kSvcFound) nx = cur;
-        RecWords rn = load(nx);
+        RecWords rn = load_tile(nx, lane, inf_off, hf_off);
+        prof.mark(1);
         uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
         if (keyok) {
             RecWords c1[1] = {rc};
             verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
         }
+        if constexpr (HFV_SVC_PROF) prof.c[5] += 1;
+        prof.mark(2);
         if (lane == stashed) {
             st_word = ballot;
             st_tile = cur.tile;
         }
+        st_bits = cur.bits;
         ++stashed;
         ++pending;
         const bool leave = c != kSvcFound || nx.b != cur.b;
         if (leave || stashed == 64) {
-            if (lane < stashed)
-                __hip_atomic_store(reinterpret_cast<uint64_t *>(cur.bits) + st_tile, st_word, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            stashed = 0;
+            flush = true;
+            fl_b = cur.b;
+            fl_count = cur.count;
+            fl_k = leave ? pending : 0;
+            if (leave) pending = 0;
         }
-        if (leave) {
-            svc_count(host, lane, cur.b, cur.count, pending);
-            pending = 0;
+        prof.mark(3);
+        if (c != kSvcFound) {
+            // before waiting for the host (or leaving): store and count everything verified,
+            // so a host that waits for those batches before posting the next never waits on us
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            count(dc_b, dc_count, dc_k);
+            dc_k = 0;
+            if (flush) {
+                store_stash();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                count(fl_b, fl_count, fl_k);
+                flush = false;
+            }
+            if (c == kSvcPending) {
+                c = svc_map(host, mir, idle_ticks, lane, g, true, mb, none, nx);
+                if (c == kSvcFound) rn = load_tile(nx, lane, inf_off, hf_off);
+            }
         }
-        if (c == kSvcPending) {
-            c = svc_map(host, mir, idle_ticks, lane, g, true, mb, none, nx);
-            if (c == kSvcFound) rn = load(nx);
-        }
+        prof.mark(4);
         if (c == kSvcStop) break;
         if (nx.b != cur.b) svc_prefetch(host, mir, idle_ticks, lane, nx.b);
         cur = nx;
         rc = rn;
     }
+    prof.flush(host, lane, prof_t0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         __hip_atomic_store(&host->run_clock[2], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&host->run_clock[3], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,

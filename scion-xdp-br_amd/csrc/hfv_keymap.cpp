@@ -196,6 +196,13 @@ int hfv_keymap_erase(const char *path, uint32_t index)
     return rc;
 }
 
+int hfv_keymap_create(const char *path)
+{
+    if (!path) return fail(-EINVAL, "null argument");
+    int rc = keymap_create(path);
+    return rc ? fail(rc, "cannot create key map %s", path) : 0;
+}
+
 int hfv_keymap_read(const char *path, struct hop_key *slots, uint32_t *valid)
 {
     if (!path || !slots || !valid) return fail(-EINVAL, "null argument");

@@ -6,10 +6,20 @@
 //   hfv-loader key list <br>                        print occupied slots and K1 of each
 //   hfv-loader watch <br> <iface> [seconds]         verdict counters of one ingress port,
 //                                                   every second (br_loader.cpp:162-180)
+//   hfv-loader attach <config> [--route R]...       loadConfig + initializeMaps + pin
+//                                                   (attachBr, br_loader.cpp:88-151): print the
+//                                                   configuration, publish the router tables to
+//                                                   $HFV_PIN_DIR/<self>/br_config, create (or
+//                                                   reuse) the pinned key and counter maps.
+//                                                   R = <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]
+//                                                   is one static next hop (bpf_fib_lookup has no
+//                                                   GPU counterpart)
+//   hfv-loader detach <br>                          unpublish the router tables (detachBr)
 //
 // The pinned map lives at $HFV_PIN_DIR/<br>/mac_key_map (default /dev/shm/hfv); a data plane
 // that called hfv_ctx_attach_keymap() on it picks the change up at its next batch.  Messages
 // and exit codes follow br-loader: errors on stderr, EXIT_FAILURE.
+#include <arpa/inet.h>
 #include <net/if.h>
 #include <signal.h>
 #include <stdio.h>
@@ -29,7 +39,9 @@ static void print_usage()
             "Usage: hfv-loader key add <br> <index> <key>\n"
             "                  key remove <br> <index>\n"
             "                  key list <br>\n"
-            "       hfv-loader watch <br> <iface> [seconds]\n");
+            "       hfv-loader watch <br> <iface> [seconds]\n"
+            "       hfv-loader attach <config> [--route <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]]...\n"
+            "                  detach <br>\n");
 }
 
 static bool parse_index(const char *s, uint32_t *out)
@@ -201,8 +213,119 @@ static int watch(int argc, char **argv)
     return EXIT_SUCCESS;
 }
 
+// ---- attach / detach (br_loader.cpp:88-160) ---------------------------------------------
+static bool parse_mac(const char *s, uint8_t out[6])
+{
+    unsigned v[6];
+    if (sscanf(s, "%x:%x:%x:%x:%x:%x", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]) != 6) return false;
+    for (int i = 0; i < 6; ++i) {
+        if (v[i] > 255) return false;
+        out[i] = (uint8_t)v[i];
+    }
+    return true;
+}
+
+// <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]
+static bool parse_route(const char *arg, struct hfv_br_next_hop *h)
+{
+    memset(h, 0, sizeof *h);
+    std::string a(arg);
+    std::string f[5];
+    int n = 0;
+    size_t pos = 0;
+    while (n < 5) {
+        size_t c = a.find(',', pos);
+        f[n++] = a.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    if (n < 4) return false;
+    size_t slash = f[0].find('/');
+    if (slash == std::string::npos) return false;
+    std::string ip = f[0].substr(0, slash);
+    uint32_t plen;
+    if (!parse_index(f[0].c_str() + slash + 1, &plen)) return false;
+    if (inet_pton(AF_INET, ip.c_str(), h->prefix) == 1) h->family = HFV_AF_INET;
+    else if (inet_pton(AF_INET6, ip.c_str(), h->prefix) == 1) h->family = HFV_AF_INET6;
+    else return false;
+    if (plen > (h->family == HFV_AF_INET ? 32u : 128u) || f[1].empty() || f[1].size() >= sizeof h->ifname) return false;
+    h->prefix_len = plen;
+    memcpy(h->ifname, f[1].c_str(), f[1].size());
+    if (!parse_mac(f[2].c_str(), h->smac) || !parse_mac(f[3].c_str(), h->dmac)) return false;
+    if (n == 5) h->ret = atoi(f[4].c_str());
+    return true;
+}
+
+static int attach(int argc, char **argv)
+{
+    if (argc < 1) { print_usage(); return EXIT_FAILURE; }
+    static struct hfv_br_next_hop hops[HFV_BR_MAX_ROUTES];
+    size_t nh = 0;
+    for (int i = 1; i < argc; ++i) {
+        if (strcmp(argv[i], "--route") == 0 && i + 1 < argc && nh < HFV_BR_MAX_ROUTES && parse_route(argv[i + 1], &hops[nh])) {
+            ++nh;
+            ++i;
+            continue;
+        }
+        fprintf(stderr, "Invalid argument: %s\n", argv[i]);
+        print_usage();
+        return EXIT_FAILURE;
+    }
+    static struct hfv_br_config cfg;
+    static char self[256], listing[65536], diag[65536];
+    int rc = hfv_br_config_load(argv[0], nullptr, 0, hops, nh, &cfg, self, sizeof self, listing, sizeof listing,
+                                diag, sizeof diag);
+    fputs(diag, stderr);
+    if (rc) return EXIT_FAILURE;
+    fputs(listing, stdout);
+    char kpath[4096], spath[4096], cpath[4096];
+    if (hfv_keymap_path(self, kpath, sizeof kpath) || hfv_statsmap_path(self, spath, sizeof spath) ||
+        hfv_brconfig_path(self, cpath, sizeof cpath)) {
+        fprintf(stderr, "Invalid border router name: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
+    // reusePinnedMap: keys and counters survive a re-attach (br_loader.cpp:119-126)
+    if (access(kpath, F_OK) == 0) printf("Reusing pinned map: \"%s\"\n", kpath);
+    else if (hfv_keymap_create(kpath) != 0) {
+        fprintf(stderr, "Cannot create key map: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
+    if (access(spath, F_OK) == 0) printf("Reusing pinned map: \"%s\"\n", spath);
+    else {
+        static uint64_t zero[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+        if (hfv_statsmap_add(spath, zero) != 0) {
+            fprintf(stderr, "Cannot create counter map: %s\n", hfv_last_error());
+            return EXIT_FAILURE;
+        }
+    }
+    if (hfv_brconfig_publish(cpath, &cfg) != 0) {
+        fprintf(stderr, "Cannot publish router tables: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
+    printf("HFV-BR attached: %s\n", cpath);
+    return EXIT_SUCCESS;
+}
+
+static int detach(int argc, char **argv)
+{
+    if (argc < 1) { print_usage(); return EXIT_FAILURE; }
+    char cpath[4096];
+    if (hfv_brconfig_path(argv[0], cpath, sizeof cpath) != 0) {
+        fprintf(stderr, "Invalid border router name: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
+    if (unlink(cpath) != 0) {
+        fprintf(stderr, "Not attached: %s\n", cpath);
+        return EXIT_FAILURE;
+    }
+    printf("HFV-BR detached\n");
+    return EXIT_SUCCESS;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc >= 2 && strcmp(argv[1], "attach") == 0) return attach(argc - 2, argv + 2);
+    if (argc >= 2 && strcmp(argv[1], "detach") == 0) return detach(argc - 2, argv + 2);
     if (argc >= 2 && strcmp(argv[1], "watch") == 0) return watch(argc - 2, argv + 2);
     if (argc >= 3 && strcmp(argv[1], "key") == 0) {
         if (strcmp(argv[2], "add") == 0) return add_key(argc - 3, argv + 3);

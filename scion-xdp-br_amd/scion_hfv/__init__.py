@@ -77,6 +77,13 @@ def lib():
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
         "hfv_br_set_hf_check": (i32, [vp, i32]),
+        "hfv_br_config_load": (i32, [ctypes.c_char_p, vp, sz, vp, sz, vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
+                                     ctypes.c_char_p, sz]),
+        "hfv_br_load_config": (i32, [vp, ctypes.c_char_p, vp, sz]),
+        "hfv_brconfig_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
+        "hfv_brconfig_publish": (i32, [ctypes.c_char_p, vp]),
+        "hfv_brconfig_read": (i32, [ctypes.c_char_p, vp]),
+        "hfv_ctx_attach_brconfig": (i32, [vp, ctypes.c_char_p]),
         "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_br_process_host": (i32, [vp, vp, sz, vp, vp, sz, sz, vp, vp, vp, vp]),
@@ -306,6 +313,10 @@ class Ctx:
     def br_set_config(self, cfg):
         _check(lib().hfv_br_set_config(self._h, ctypes.byref(cfg)))
 
+    def attach_brconfig(self, path):
+        """Use the pinned router tables at `path` (hfv-loader attach), reloaded when republished."""
+        _check(lib().hfv_ctx_attach_brconfig(self._h, path.encode()))
+
     def br_set_hf_check(self, enable: bool):
         """ENABLE_HF_CHECK on/off (br/CMakeLists.txt:8): off skips the hop-field MAC check."""
         _check(lib().hfv_br_set_hf_check(self._h, 1 if enable else 0))
@@ -358,17 +369,25 @@ class Ctx:
         _check(lib().hfv_service_submit(self._h, _ptr(recs), stride, n, _ptr(pass_bits), ctypes.byref(t)))
         return t.value
 
-    def service_submitv(self, batches):
-        """Post several batches in one call: batches = [(recs, n, pass_bits[, stride]), ...];
-        returns their tickets."""
+    @staticmethod
+    def service_batches(batches):
+        """A struct hfv_batch array for service_submitv, built once (batches = [(recs, n,
+        pass_bits[, stride]), ...]): posting it then costs one C call."""
         arr = (HfvBatch * len(batches))()
         for i, b in enumerate(batches):
             recs, n, bits = b[0], b[1], b[2]
             arr[i].recs, arr[i].n, arr[i].pass_bits = _ptr(recs), n, _ptr(bits)
             arr[i].stride = b[3] if len(b) > 3 else REC_SIZE
+        return arr
+
+    def service_submitv(self, batches):
+        """Post several batches in one call (a list as for service_batches, or its result);
+        starts the service if needed, launching its grid after the batches are in the ring.
+        Returns their tickets."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
         t = ctypes.c_uint64()
-        _check(lib().hfv_service_submitv(self._h, arr, len(batches), ctypes.byref(t)))
-        return list(range(t.value, t.value + len(batches)))
+        _check(lib().hfv_service_submitv(self._h, arr, len(arr), ctypes.byref(t)))
+        return list(range(t.value, t.value + len(arr)))
 
     def service_poll(self, ticket):
         rc = lib().hfv_service_poll(self._h, ticket)
@@ -388,13 +407,26 @@ class Ctx:
     def service_shader_mhz(self):
         """Diagnostic: block 0's shader clock over the last service grid's life (s_memtime
         against the 100 MHz s_memrealtime), or None."""
-        clk = (ctypes.c_uint64 * (SVC_RING + 4))()
+        clk = (ctypes.c_uint64 * (2 * SVC_RING + 4))()
         L = lib()
         L.hfv_debug_service_clocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         if L.hfv_debug_service_clocks(self._h, clk) != 0:
             return None
         t0, r0, t1, r1 = (int(x) for x in clk[SVC_RING:SVC_RING + 4])
         return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
+
+    def service_timeline(self, nbatches):
+        """Diagnostic: per batch of the last grid, (relay published, block 0 loaded) in us
+        after block 0's loop start, and the grid's loop span."""
+        clk = (ctypes.c_uint64 * (2 * SVC_RING + 4))()
+        L = lib()
+        L.hfv_debug_service_clocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        if L.hfv_debug_service_clocks(self._h, clk) != 0:
+            return None
+        r0, r1 = int(clk[SVC_RING + 1]), int(clk[SVC_RING + 3])
+        us = lambda t: round((int(t) - r0) / 100.0, 2) if t else None   # noqa: E731
+        return {"loop_us": us(r1), "relay_us": [us(clk[SVC_RING + 4 + i]) for i in range(nbatches + 1)],
+                "load_us": [us(clk[i]) for i in range(nbatches + 1)]}
 
     @property
     def service_running(self):
@@ -497,6 +529,64 @@ class BrConfig(ctypes.Structure):
     def add_tx_port(self, ifindex):
         self.tx_ports[self.n_tx_ports] = ifindex
         self.n_tx_ports += 1
+
+
+class BrIfAddr(ctypes.Structure):
+    """struct hfv_br_ifaddr: one address of the getifaddrs view."""
+    _fields_ = [("ifname", ctypes.c_char * 16), ("ifindex", ctypes.c_uint32), ("family", ctypes.c_uint32),
+                ("addr", ctypes.c_uint8 * 16)]
+
+
+class BrNextHop(ctypes.Structure):
+    """struct hfv_br_next_hop: one static FIB entry (replaces bpf_fib_lookup)."""
+    _fields_ = [("family", ctypes.c_uint32), ("prefix", ctypes.c_uint8 * 16), ("prefix_len", ctypes.c_uint32),
+                ("ifname", ctypes.c_char * 16), ("smac", ctypes.c_uint8 * 6), ("dmac", ctypes.c_uint8 * 6),
+                ("ret", ctypes.c_int32)]
+
+
+def br_config_load(toml_path, if_addrs=None, ifindex_of=None, next_hops=()):
+    """br-loader's loadConfig + initializeMaps in the C library (hfv_br_config_load).
+    if_addrs: {ip: ifname} (None: this namespace); ifindex_of: ifname -> ifindex for if_addrs;
+    next_hops: (prefix, prefix_len, ifname, smac, dmac[, ret]).
+    Returns (rc, BrConfig, self, listing, diag)."""
+    ifs = None
+    n_ifs = 0
+    if if_addrs is not None:
+        ifs = (BrIfAddr * max(1, len(if_addrs)))()
+        for k, (ip, name) in enumerate(if_addrs.items()):
+            fam, a = BrConfig._ip(str(ip))
+            ifs[k].ifname, ifs[k].family, ifs[k].addr = name.encode(), fam, a
+            ifs[k].ifindex = ifindex_of(name) if ifindex_of else 0
+        n_ifs = len(if_addrs)
+    hops = (BrNextHop * max(1, len(next_hops)))()
+    for k, h in enumerate(next_hops):
+        prefix, plen, ifname, smac, dmac = h[:5]
+        hops[k].family, hops[k].prefix = BrConfig._ip(prefix)
+        hops[k].prefix_len, hops[k].ifname = plen, ifname.encode()
+        hops[k].smac, hops[k].dmac = BrConfig._mac(smac), BrConfig._mac(dmac)
+        hops[k].ret = h[5] if len(h) > 5 else 0
+    cfg = BrConfig()
+    selfb, lst, diag = (ctypes.create_string_buffer(256), ctypes.create_string_buffer(16384),
+                        ctypes.create_string_buffer(16384))
+    rc = lib().hfv_br_config_load(str(toml_path).encode(), ifs, n_ifs, hops, len(next_hops), ctypes.byref(cfg),
+                                  selfb, 256, lst, 16384, diag, 16384)
+    return rc, cfg, selfb.value.decode(), lst.value.decode(), diag.value.decode()
+
+
+def brconfig_path(br: str) -> str:
+    buf = ctypes.create_string_buffer(4096)
+    _check(lib().hfv_brconfig_path(br.encode(), buf, 4096))
+    return buf.value.decode()
+
+
+def brconfig_publish(path: str, cfg):
+    _check(lib().hfv_brconfig_publish(path.encode(), ctypes.byref(cfg)))
+
+
+def brconfig_read(path: str):
+    cfg = BrConfig()
+    _check(lib().hfv_brconfig_read(path.encode(), ctypes.byref(cfg)))
+    return cfg
 
 
 # enum verdict (br/src/bpf/common.h:55-70)

@@ -86,3 +86,46 @@ def test_statsmap_and_watch(pin_dir):
     assert r.returncode == 1 and "Lookup failed" in r.stderr
     with pytest.raises(hfv.HfvError):
         hfv.statsmap_read(str(pin_dir / "missing" / "port_stats_map"))
+
+
+def test_cli_attach_detach(pin_dir, tmp_path):
+    """`hfv-loader attach <config> [--route ...]` (attachBr, br_loader.cpp:88-151): prints the
+    configuration listing, publishes the router tables under $HFV_PIN_DIR/<self>/br_config,
+    creates the pinned key and counter maps (reused on a second attach); `detach <br>` removes
+    the tables.  The tables are the ones hfv_br_config_load builds (checked against the Python
+    loader in test_br_config.py)."""
+    if not os.path.exists(LOADER):
+        pytest.skip("hfv-loader not built")
+    import json
+    topo = {"border_routers": {"br1-x": {"internal_addr": "10.2.0.1:31002", "interfaces": {
+        "1": {"underlay": {"public": "10.1.1.2:50000", "remote": "10.1.1.1:50000"}}}},
+        "br2-x": {"internal_addr": "10.2.0.0:31002", "interfaces": {"3": {"underlay": {
+            "public": "10.1.3.2:50000", "remote": "10.1.3.1:50000"}}}}}}
+    tp = tmp_path / "topology.json"
+    tp.write_text(json.dumps(topo))
+    conf = tmp_path / "br1.toml"
+    conf.write_text('self = "br1-x"\ntopology = "%s"\ninternal_interfaces = [\n    {ip = "10.2.0.1", port = 31002}\n]\n' % tp)
+    env = dict(os.environ)
+    r = run("attach", str(conf), "--route", "10.1.1.0/24,lo,02:00:00:00:00:01,02:00:00:00:00:02", env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("XDP Border Router br1-x\nExternal interfaces:\n")
+    assert "WARNING: No interface has IP 10.1.1.2" in r.stderr        # not this namespace's address
+    cpath = hfv.brconfig_path("br1-x")
+    assert "HFV-BR attached: %s" % cpath in r.stdout
+    cfg = hfv.brconfig_read(cpath)
+    assert cfg.n_egress == 2 and cfg.n_routes == 1 and cfg.routes[0].prefix_len == 24
+    assert os.path.exists(hfv.keymap_path("br1-x")) and os.path.exists(hfv.statsmap_path("br1-x"))
+    assert hfv.keymap_read(hfv.keymap_path("br1-x")) == {}
+    r = run("key", "add", "br1-x", "0", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert r.returncode == 0
+    r = run("attach", str(conf), env=env)                             # re-attach keeps the keys
+    assert r.returncode == 0 and r.stdout.count("Reusing pinned map") == 2
+    assert sorted(hfv.keymap_read(hfv.keymap_path("br1-x"))) == [0]
+    assert hfv.brconfig_read(cpath).n_routes == 0
+    bad = run("attach", str(conf), "--route", "10.1.1.0/99,lo,aa,bb", env=env)
+    assert bad.returncode != 0 and "Invalid argument" in bad.stderr
+    bad = run("attach", str(tmp_path / "missing.toml"), env=env)
+    assert bad.returncode != 0 and "Parsing configuration failed" in bad.stderr
+    assert run("detach", "br1-x", env=env).returncode == 0
+    assert not os.path.exists(cpath)
+    assert run("detach", "br1-x", env=env).returncode != 0

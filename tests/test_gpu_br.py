@@ -208,3 +208,44 @@ def test_host_path_survives_keymap_attach(gpu_ctx, tmp_path, monkeypatch):
         if not attach:
             gpu_ctx.attach_keymap(hfv.keymap_path("br1"))   # an empty map: re-add the key through it
             gpu_ctx.key_add(0, T.KEYS[1])
+
+
+def test_attached_pinned_brconfig_reloads(gpu_ctx, tmp_path, monkeypatch):
+    """hfv_ctx_attach_brconfig: the data plane takes its router tables from the pinned file
+    `hfv-loader attach` publishes and picks up a republished version at the next batch."""
+    monkeypatch.setenv("HFV_PIN_DIR", str(tmp_path))
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, False, MAC)
+    frames, lens, ifidx = F.fuzz_batch(hops, "br1", False, 3000, seed=31)
+    path = hfv.brconfig_path("br1-ff00_0_1-1")
+    hfv.brconfig_publish(path, T.br_config("br1"))
+    import ctypes
+    import torch
+
+    class Pinned(T.GpuBR):   # like GpuBR, but without installing tables itself
+        def process(self, frames, lens, ifidx):
+            ctx = self.ctx
+            ctx.key_add(0, T.KEYS[1])
+            n, slot = frames.shape
+            d = torch.from_numpy(frames).cuda()
+            dl = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).cuda()
+            di = torch.from_numpy(ifidx.astype(np.uint32).view(np.int32)).cuda()
+            a = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            v = torch.zeros_like(a)
+            e = torch.zeros(n, dtype=torch.int32, device="cuda")
+            ctx.br_process(d, slot, dl, di, n, a, v, e)
+            torch.cuda.synchronize()
+            frames[:] = d.cpu().numpy()
+            return a.cpu().numpy(), v.cpu().numpy(), e.cpu().numpy()
+
+    gpu_ctx.br_set_config(hfv.BrConfig())          # empty tables: the attach must replace them
+    gpu_ctx.br_set_hf_check(True)
+    gpu_ctx.attach_brconfig(path)
+    for cfg_name in ("br1", "br2"):
+        hfv.brconfig_publish(path, T.br_config(cfg_name))
+        ref = frames.copy()
+        oa, ov, oe, _ = orc.br_process(ref, lens, ifidx, T.br_config(cfg_name), orc.hop_key(T.KEYS[1]))
+        got = frames.copy()
+        ga, gv, ge = Pinned(gpu_ctx, None).process(got, lens, ifidx)
+        assert (ga == oa).all() and (gv == ov).all() and (ge == oe).all() and (got == ref).all(), cfg_name
+    assert ctypes.sizeof(hfv.BrConfig) > 0

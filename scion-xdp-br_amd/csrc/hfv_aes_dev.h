@@ -109,6 +109,21 @@ __device__ __forceinline__ void fill_ttab_dma_issue(const uint32_t *__restrict__
     }
 }
 
+// Issue-only form for `nw` filling waves (wave index `wave` < nw) of a block some of whose
+// waves do other work.
+template <int TAB>
+__device__ __forceinline__ void fill_ttab_dma_issue_n(const uint32_t *__restrict__ img, uint32_t wave, uint32_t nw)
+{
+    constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    const int lane = threadIdx.x & 63;
+    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
+    for (uint32_t c = wave; c < kChunks; c += nw) {
+        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
+    }
+}
+
 template <int TAB>
 __device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
 {
@@ -126,10 +141,12 @@ __device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__device__ __forceinline__ void fill_keys(const DevKeyTable *tab)
+// nthr: the block's threads 0..nthr-1 share the copy (0: all of them)
+__device__ __forceinline__ void fill_keys(const DevKeyTable *tab, uint32_t nthr = 0)
 {
+    const uint32_t n = nthr ? nthr : blockDim.x;
     const uint4 *src = reinterpret_cast<const uint4 *>(tab->rows);
-    for (int e = threadIdx.x; e < kDevKeyRows * HFV_MAX_KEYS; e += blockDim.x) s_keys[e] = src[e];
+    for (uint32_t e = threadIdx.x; e < kDevKeyRows * HFV_MAX_KEYS; e += n) s_keys[e] = src[e];
     if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
 }
 

@@ -1379,8 +1379,24 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     int rc = 0;
     if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0)
         rc = svc_post(ctx, 0, 0, kSvcStopN, 0, nullptr);
-    // the grid exits on the stop descriptor, or on its idle timeout if the post failed
-    hipError_t e = hipStreamSynchronize(ctx->svc_stream);
+    // the grid exits on the stop descriptor, or on its idle timeout if the post failed.  Spin
+    // on the stream for a while first: the blocking wait sleeps on an interrupt, whose wake-up
+    // costs more than the last batches of a short run.
+    hipError_t e = hipErrorNotReady;
+    struct timespec t0, now;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint64_t spin = 0;; ++spin) {
+        e = hipStreamQuery(ctx->svc_stream);
+        if (e != hipErrorNotReady) break;
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 1023) {
+            clock_gettime(CLOCK_MONOTONIC, &now);
+            if ((now.tv_sec - t0.tv_sec) * 1000000000ll + (now.tv_nsec - t0.tv_nsec) > 20000000ll) {   // 20 ms
+                e = hipStreamSynchronize(ctx->svc_stream);
+                break;
+            }
+        }
+    }
     ctx->svc_running = false;
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;

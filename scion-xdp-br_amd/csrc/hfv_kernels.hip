@@ -741,13 +741,13 @@ __device__ void svc_complete(SvcShared *host, uint32_t b)
 // PCIe reads cost 25-35 us per batch (svc_probe: grid 32/128/256 -> 75/36/45 us per 2^20
 // batch against an 11 us compute bound).  The relay also owns the idle timeout: after
 // idle_ticks without a new host post it publishes a stop descriptor.
-__device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks)
+__device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks, uint64_t tag)
 {
     for (uint32_t b = 0;; ++b) {
         const uint32_t slot = b % kSvcRing;
         SvcDesc *h = &host->desc[slot];
         bool idle = false;
-        const uint64_t want = s_svc_tag | ((uint64_t)b + 1);
+        const uint64_t want = tag | ((uint64_t)b + 1);
         if (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
@@ -955,14 +955,20 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         s_svc_lock = 0;
         s_svc_tag = tag;
     }
-    fill_ttab_dma_issue<TAB, 1024>(ttab_img);
+    // Block 0's last wave relays the host's descriptors into device memory for the grid's
+    // whole life.  It must not be alive at a barrier the other waves wait at (a wave still
+    // running holds the barrier), so it passes the table-fill barrier without filling and
+    // starts relaying right after it.
+    const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
+    const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
+    if (!relay) fill_ttab_dma_issue_n<TAB>(ttab_img, threadIdx.x >> 6, nthr >> 6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
+    if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
+        if (!relay) fill_keys(tab, nthr);
+    }
     __syncthreads();
-    // block 0's last wave relays the host's descriptors into device memory (no barrier
-    // follows, so the block's other waves go on without it)
-    if (blockIdx.x == 0 && threadIdx.x / 64 == blockDim.x / 64 - 1) {
-        if (lane == 0) svc_relay(host, mir, idle_ticks);
+    if (relay) {   // no barrier follows: the block's other waves go on without it
+        if (lane == 0) svc_relay(host, mir, idle_ticks, tag);
         return;
     }
     const Lane l = lane_bases();

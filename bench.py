@@ -643,6 +643,51 @@ def host_leg(hfv, W, ctx, recs, n, ref_bits):
                                            "whole 64 B lines), bitmap written to registered host memory"}}
 
 
+def measure_loop(hfv, W, total, chunk, chunks, producers, consumers):
+    """Config 5 in one process (hfv_loop_run): gen_packets.py's 1000 frames cycled by producer
+    threads into a registered RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each
+    chunk zero-copy, consumer threads counting transmitted frames and dropping the rest."""
+    from scion_hfv import evaluation as E
+    ctx = hfv.Ctx(W.device)
+    E.setup_ctx(ctx)
+    frames = E.frames(1000)
+    lens = np.full(1000, E.FRAME_LEN, dtype=np.uint16)
+    kw = dict(rx_ifindex=E.RX_IFINDEX, slot=192, chunk=chunk, chunks=chunks, producers=producers,
+              consumers=consumers)
+    ctx.loop_run(frames, lens, 4 * chunk, **kw)                          # warm the registration path
+    W.barrier()
+    r = ctx.loop_run(frames, lens, total, **kw)
+    el = max(W.gather(r["seconds"]))
+    assert r["rx"] == total and r["tx"] == total and r["verdicts"][1] == total, r   # every frame forwarded
+    r["numa_node"] = ctx.numa_node()
+    ctx.close()
+    return {"mpkts": round(W.size * total / el / 1e6, 2), "seconds": round(el, 4), "frames_per_gpu": total,
+            "chunk": chunk, "chunks": chunks, "producers": producers, "consumers": consumers,
+            "tx_gbit_s": round(W.size * total * E.FRAME_LEN * 8 / el / 1e9, 1), "numa_node": r.get("numa_node"),
+            "path": "producer threads memcpy 138 B frames into a registered host RX ring (192 B slots) -> "
+                    "hfv_br_process_host zero-copy per chunk (kernel reads headers over PCIe, writes rewritten "
+                    "rows back) -> consumer threads count TX / drop; producers and consumers on the GPU's NUMA node",
+            "veth": "not used: `ip link add type veth` needs CAP_NET_ADMIN, which neither this container nor the "
+                    "GPU box grants (DESIGN.md section 7)"}
+
+
+def run_loop(args, W):
+    import scion_hfv as hfv
+    r = measure_loop(hfv, W, args.loop_n, args.loop_chunk, 8, args.loop_threads, args.loop_threads)
+    result = {
+        "metric": "Mpkt/s config-5 loop: RX ring -> border router on the GPU -> TX/drop, 138 B frames",
+        "value": r["mpkts"], "unit": "Mpkt/s", "n_gpus": W.size, "steps": 1, "warmup": 1,
+        "ms_per_step": round(r["seconds"] * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (gen_packets.py's 1000 frames, cycled like tcpreplay --loop)",
+        "config": {"workload": f"config 5: {args.loop_n} frames per GPU through hfv_loop_run as br1-ff00_0_1-2",
+                   "parallelism": f"one loop per GPU x{W.size}, no collective"},
+        "loop": r,
+    }
+    if W.rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def run_dry(args, W):
     """Launcher check without a GPU: every rank times K trivial CPU steps."""
     x = np.arange(1 << 12, dtype=np.uint64)
@@ -810,6 +855,11 @@ def run_hf(args, W):
                              "note": "hf_check_off = the reference's ENABLE_HF_CHECK=OFF build (br/CMakeLists.txt:8,"
                                      "48-64); hf_check_share = the part of the kernel time the MAC check costs"}
 
+    if extras and args.loop_n:
+        W.sync()
+        result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, 8, args.loop_threads,
+                                              args.loop_threads)
+
     if W.rank == 0 and W.size == 1 and args.cpu_budget > 0:
         result["cpu_baseline"] = cpu_baseline(recs0.cpu().numpy(), keysel, ref_bits, args.cpu_budget)
 
@@ -834,9 +884,12 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of multi-thread CPU baseline (0 = skip)")
     ap.add_argument("--no-host-e2e", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (no config 3/4, 2^24, MALL legs)")
-    ap.add_argument("--workload", choices=["hf", "br", "br-host"], default="hf",
+    ap.add_argument("--workload", choices=["hf", "br", "br-host", "loop"], default="hf",
                     help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
-                         "br-host: config 5 router leg")
+                         "br-host: config 5 router leg; loop: config 5 RX ring -> router -> TX loop")
+    ap.add_argument("--loop-n", type=int, default=1 << 23, help="config-5 loop frames (0 = skip the leg)")
+    ap.add_argument("--loop-chunk", type=int, default=1 << 16, help="config-5 loop frames per chunk")
+    ap.add_argument("--loop-threads", type=int, default=4, help="config-5 loop producer and consumer threads each")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--launch-only", action="store_true",
@@ -849,9 +902,9 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="launcher check: gloo ranks, no GPU work")
     args = ap.parse_args()
     if args.steps is None:
-        args.steps = {"hf": 200, "br": 10, "br-host": 5}[args.workload]
+        args.steps = {"hf": 200, "br": 10, "br-host": 5, "loop": 1}[args.workload]
     if args.warmup is None:
-        args.warmup = {"hf": 20, "br": 3, "br-host": 1}[args.workload]
+        args.warmup = {"hf": 20, "br": 3, "br-host": 1, "loop": 1}[args.workload]
     if args.same_device:
         args.dist_backend = "gloo"
         args.launch_only = True
@@ -865,6 +918,8 @@ def main():
             run_br(args, W)
         elif args.workload == "br-host":
             run_br_host(args, W)
+        elif args.workload == "loop":
+            run_loop(args, W)
         else:
             run_hf(args, W)
     finally:

@@ -273,7 +273,8 @@ struct hfv_br_config {
     uint32_t tx_ports[HFV_BR_MAX_TXPORTS];   /* tx_port_map: ifindices a redirect may target */
 };
 
-/* Install the router tables (copied; takes effect for batches enqueued afterwards). */
+/* Install the router tables (copied; takes effect for batches enqueued afterwards).  Detaches
+ * a pinned config attached with hfv_ctx_attach_brconfig. */
 int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
 /* The reference's ENABLE_HF_CHECK build switch (br/CMakeLists.txt:8,48-64) as a runtime
  * setting: enable = 0 skips the hop-field MAC check (defer_verify_hop_field and the MAC block
@@ -357,6 +358,34 @@ int hfv_statsmap_read(const char *path, uint64_t *stats);
  * (`window` is then unused); registered len/ifindex/output arrays are used in place. */
 int hfv_host_register(hfv_ctx *ctx, void *ptr, size_t bytes);
 int hfv_host_unregister(hfv_ctx *ctx, void *ptr);
+
+/* ---- config 5 in one process (br/evaluation/README.md:131-139) --------------------------
+ * The reference measures its router with tcpreplay pushing gen_packets.py's frames into a veth
+ * pair, the XDP program on the other end, and count_and_drop.py on the TX side.  hfv_loop_run
+ * is that loop without the kernel's network stack: producer threads copy the frame list
+ * (cycling, like `tcpreplay --loop`) into a registered RX ring of `chunks` x `chunk` slots,
+ * the calling thread runs hfv_br_process_host zero-copy over each filled chunk, and consumer
+ * threads "transmit" redirected frames (count, bytes, optional digest) and drop the rest.
+ * Producers and consumers run on the GPU's NUMA node. */
+struct hfv_loop_config {
+    const uint8_t *frames;       /* n_frames frames, frame_stride bytes apart */
+    const uint16_t *lens;
+    size_t n_frames, frame_stride;
+    uint32_t rx_ifindex;         /* ingress interface of every frame */
+    uint32_t slot;               /* ring slot bytes (multiple of 64, >= every len) */
+    size_t chunk, chunks;        /* frames per chunk, chunks in the ring (>= 2) */
+    uint64_t total;              /* frames to push through */
+    int producers, consumers;    /* threads per side (0: 1) */
+    int digest;                  /* 1: sum a 64-bit digest of every transmitted frame + egress */
+    uint64_t *stats;             /* nullable: per-ifindex verdict counters, as hfv_br_process_host */
+};
+struct hfv_loop_stats {
+    uint64_t rx_pkts, tx_pkts, tx_bytes, drop_pkts;
+    uint64_t tx_digest;                         /* sum over transmitted frames (order-free) */
+    uint64_t verdict_pkts[HFV_BR_COUNTERS];     /* frames per final verdict counter (verdict >> 3) */
+    double seconds;                             /* wall time of the whole loop */
+};
+int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *cfg, struct hfv_loop_stats *out);
 
 /* Same, then waits for the launch and returns its execution time (start/stop of the kernel
  * dispatch itself) in *kernel_ms.  For benchmarks. */

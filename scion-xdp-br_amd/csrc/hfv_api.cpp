@@ -693,6 +693,8 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
     compile_br_config(cfg, &ctx->br);
     ctx->br.hf_check_off = off;
     ctx->dirty = true;
+    brcfg_close(ctx->brmap);   // explicit tables replace an attached pinned config
+    ctx->brmap = nullptr;
     return 0;
 }
 

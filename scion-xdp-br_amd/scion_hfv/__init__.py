@@ -88,6 +88,7 @@ def lib():
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_br_process_host": (i32, [vp, vp, sz, vp, vp, sz, sz, vp, vp, vp, vp]),
         "hfv_host_register": (i32, [vp, vp, sz]),
+        "hfv_loop_run": (i32, [vp, vp, vp]),
         "hfv_statsmap_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
         "hfv_statsmap_add": (i32, [ctypes.c_char_p, vp]),
         "hfv_statsmap_read": (i32, [ctypes.c_char_p, vp]),
@@ -208,6 +209,36 @@ class HfvBatch(ctypes.Structure):
     """struct hfv_batch (hfv_service_submitv)"""
     _fields_ = [("recs", ctypes.c_void_p), ("stride", ctypes.c_size_t), ("n", ctypes.c_size_t),
                 ("pass_bits", ctypes.c_void_p)]
+
+
+class LoopConfig(ctypes.Structure):
+    """struct hfv_loop_config"""
+    _fields_ = [("frames", ctypes.c_void_p), ("lens", ctypes.c_void_p), ("n_frames", ctypes.c_size_t),
+                ("frame_stride", ctypes.c_size_t), ("rx_ifindex", ctypes.c_uint32), ("slot", ctypes.c_uint32),
+                ("chunk", ctypes.c_size_t), ("chunks", ctypes.c_size_t), ("total", ctypes.c_uint64),
+                ("producers", ctypes.c_int), ("consumers", ctypes.c_int), ("digest", ctypes.c_int),
+                ("stats", ctypes.c_void_p)]
+
+
+class LoopStats(ctypes.Structure):
+    """struct hfv_loop_stats"""
+    _fields_ = [("rx_pkts", ctypes.c_uint64), ("tx_pkts", ctypes.c_uint64), ("tx_bytes", ctypes.c_uint64),
+                ("drop_pkts", ctypes.c_uint64), ("tx_digest", ctypes.c_uint64),
+                ("verdict_pkts", ctypes.c_uint64 * 11), ("seconds", ctypes.c_double)]
+
+
+def loop_frame_digest(frame: bytes, egress: int) -> int:
+    """The digest hfv_loop_run sums over transmitted frames (hfv_loop.cpp frame_hash)."""
+    M = (1 << 64) - 1
+    n = len(frame)
+    h = 0x9E3779B97F4A7C15 ^ ((egress & 0xFFFFFFFF) << 32) ^ n
+    i = 0
+    while i + 8 <= n:
+        h = ((h ^ int.from_bytes(frame[i:i + 8], "little")) * 0xBF58476D1CE4E5B9) & M
+        h ^= h >> 29
+        i += 8
+    h = ((h ^ int.from_bytes(frame[i:], "little")) * 0x94D049BB133111EB) & M
+    return h ^ (h >> 31)
 
 
 class Ctx:
@@ -331,6 +362,22 @@ class Ctx:
         """Config 5: numpy host arrays in, results in place (hfv_br_process_host)."""
         _check(lib().hfv_br_process_host(self._h, _ptr(frames), slot, _ptr(lens), _ptr(ingress_ifindex), n, window,
                                          _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats)))
+
+    def loop_run(self, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
+                 consumers=2, digest=False, stats=None):
+        """Config 5 in one process (hfv_loop_run): `frames` (n x stride uint8) cycled into a
+        registered RX ring, the router over each chunk, TX/drop consumers.  Returns a dict."""
+        import numpy as np
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        cfg = LoopConfig(frames=frames.ctypes.data, lens=lens.ctypes.data, n_frames=frames.shape[0],
+                         frame_stride=frames.shape[1], rx_ifindex=rx_ifindex, slot=slot, chunk=chunk,
+                         chunks=chunks, total=total, producers=producers, consumers=consumers,
+                         digest=1 if digest else 0, stats=_ptr(stats))
+        st = LoopStats()
+        _check(lib().hfv_loop_run(self._h, ctypes.byref(cfg), ctypes.byref(st)))
+        return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,
+                "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds}
 
     def host_register(self, buf):
         _check(lib().hfv_host_register(self._h, _ptr(buf), buf.nbytes))

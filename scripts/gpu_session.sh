@@ -3,7 +3,8 @@
 # timeout (any status but 0, and 1 for pytest) ends the session so nothing else touches the
 # GPU afterwards.  Logs: gpurun_out/<tag>/<step>.log.
 #   scripts/gpu_session.sh <tag> step [step ...]
-# steps: test | smoke | bench | bench_quick | prof | pmc_zero | pmc_ifid | pmc_br | br | brhost | ubench_<name>
+# steps: test | smoke | bench | bench_quick | prof | pmc_zero | pmc_ifid | pmc_br | br | brhost | loop | looptest |
+#        ubench_<name>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; shift
@@ -36,6 +37,8 @@ for s in "$@"; do
     pmc_br) run pmc_br 1100 bash scripts/pmc_round.sh br || exit $? ;;
     br) run bench_br 600 python bench.py --workload br || exit $? ;;
     brhost) run bench_brhost 600 python bench.py --workload br-host || exit $? ;;
+    loop) run bench_loop 300 python bench.py --workload loop || exit $? ;;
+    looptest) run pytest_loop 300 python -u -m pytest tests/test_gpu_loop.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread || exit $? ;;
     ubench_*) run "$s" 300 "./build_ub/${s#ubench_}" || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac

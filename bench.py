@@ -643,7 +643,7 @@ def host_leg(hfv, W, ctx, recs, n, ref_bits):
                                            "whole 64 B lines), bitmap written to registered host memory"}}
 
 
-def measure_loop(hfv, W, total, chunk, chunks, producers, consumers):
+def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=192, inflight=3, dma=False):
     """Config 5 in one process (hfv_loop_run): gen_packets.py's 1000 frames cycled by producer
     threads into a registered RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each
     chunk zero-copy, consumer threads counting transmitted frames and dropping the rest."""
@@ -652,8 +652,8 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers):
     E.setup_ctx(ctx)
     frames = E.frames(1000)
     lens = np.full(1000, E.FRAME_LEN, dtype=np.uint16)
-    kw = dict(rx_ifindex=E.RX_IFINDEX, slot=192, chunk=chunk, chunks=chunks, producers=producers,
-              consumers=consumers)
+    kw = dict(rx_ifindex=E.RX_IFINDEX, slot=slot, chunk=chunk, chunks=chunks, producers=producers,
+              consumers=consumers, inflight=inflight, dma=dma)
     ctx.loop_run(frames, lens, 4 * chunk, **kw)                          # warm the registration path
     W.barrier()
     r = ctx.loop_run(frames, lens, total, **kw)
@@ -662,18 +662,25 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers):
     r["numa_node"] = ctx.numa_node()
     ctx.close()
     return {"mpkts": round(W.size * total / el / 1e6, 2), "seconds": round(el, 4), "frames_per_gpu": total,
-            "chunk": chunk, "chunks": chunks, "producers": producers, "consumers": consumers,
+            "chunk": chunk, "chunks": chunks, "producers": producers, "consumers": consumers, "slot": slot,
+            "inflight": inflight, "router_io": "DMA through HBM" if dma else "zero-copy over PCIe",
             "tx_gbit_s": round(W.size * total * E.FRAME_LEN * 8 / el / 1e9, 1), "numa_node": r.get("numa_node"),
+            "stage_busy_frac": {"router": round(r["gpu_busy_s"] / r["seconds"], 3),
+                                "router_waiting_for_rx": round(r["gpu_wait_s"] / r["seconds"], 3),
+                                "producer": round(r["producer_busy_s"] / producers / r["seconds"], 3),
+                                "consumer": round(r["consumer_busy_s"] / consumers / r["seconds"], 3)},
             "path": "producer threads memcpy 138 B frames into a registered host RX ring (192 B slots) -> "
                     "hfv_br_process_host zero-copy per chunk (kernel reads headers over PCIe, writes rewritten "
                     "rows back) -> consumer threads count TX / drop; producers and consumers on the GPU's NUMA node",
-            "veth": "not used: `ip link add type veth` needs CAP_NET_ADMIN, which neither this container nor the "
-                    "GPU box grants (DESIGN.md section 7)"}
+            "veth": "not used: the GPU box runs commands as an unprivileged user with user namespaces disabled "
+                    "(unshare -Urn: ENOSPC) and no CAP_NET_RAW (AF_PACKET: EPERM), so no veth pair can be made "
+                    "there (scripts/netns_gpu_probe.py, DESIGN.md)"}
 
 
 def run_loop(args, W):
     import scion_hfv as hfv
-    r = measure_loop(hfv, W, args.loop_n, args.loop_chunk, 8, args.loop_threads, args.loop_threads)
+    r = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads, args.loop_consumers,
+                     args.loop_slot, args.loop_inflight, args.loop_dma)
     result = {
         "metric": "Mpkt/s config-5 loop: RX ring -> border router on the GPU -> TX/drop, 138 B frames",
         "value": r["mpkts"], "unit": "Mpkt/s", "n_gpus": W.size, "steps": 1, "warmup": 1,
@@ -857,8 +864,8 @@ def run_hf(args, W):
 
     if extras and args.loop_n:
         W.sync()
-        result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, 8, args.loop_threads,
-                                              args.loop_threads)
+        result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads,
+                                              args.loop_consumers, args.loop_slot, args.loop_inflight, args.loop_dma)
 
     if W.rank == 0 and W.size == 1 and args.cpu_budget > 0:
         result["cpu_baseline"] = cpu_baseline(recs0.cpu().numpy(), keysel, ref_bits, args.cpu_budget)
@@ -889,7 +896,12 @@ def main():
                          "br-host: config 5 router leg; loop: config 5 RX ring -> router -> TX loop")
     ap.add_argument("--loop-n", type=int, default=1 << 23, help="config-5 loop frames (0 = skip the leg)")
     ap.add_argument("--loop-chunk", type=int, default=1 << 16, help="config-5 loop frames per chunk")
-    ap.add_argument("--loop-threads", type=int, default=4, help="config-5 loop producer and consumer threads each")
+    ap.add_argument("--loop-chunks", type=int, default=12, help="config-5 loop ring chunks")
+    ap.add_argument("--loop-threads", type=int, default=4, help="config-5 loop producer threads")
+    ap.add_argument("--loop-consumers", type=int, default=2, help="config-5 loop consumer threads")
+    ap.add_argument("--loop-slot", type=int, default=192, help="config-5 loop ring slot bytes")
+    ap.add_argument("--loop-inflight", type=int, default=3, help="config-5 loop chunks on the GPU at once")
+    ap.add_argument("--loop-dma", action="store_true", help="config-5 loop: chunks through HBM by DMA, not zero-copy")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--launch-only", action="store_true",

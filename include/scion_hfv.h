@@ -364,7 +364,8 @@ int hfv_host_unregister(hfv_ctx *ctx, void *ptr);
  * pair, the XDP program on the other end, and count_and_drop.py on the TX side.  hfv_loop_run
  * is that loop without the kernel's network stack: producer threads copy the frame list
  * (cycling, like `tcpreplay --loop`) into a registered RX ring of `chunks` x `chunk` slots,
- * the calling thread runs hfv_br_process_host zero-copy over each filled chunk, and consumer
+ * the calling thread runs the router over each filled chunk (zero-copy like hfv_br_process_host,
+ * or through HBM by DMA), `inflight` chunks at once on their own streams, and consumer
  * threads "transmit" redirected frames (count, bytes, optional digest) and drop the rest.
  * Producers and consumers run on the GPU's NUMA node. */
 struct hfv_loop_config {
@@ -372,18 +373,23 @@ struct hfv_loop_config {
     const uint16_t *lens;
     size_t n_frames, frame_stride;
     uint32_t rx_ifindex;         /* ingress interface of every frame */
-    uint32_t slot;               /* ring slot bytes (multiple of 64, >= every len) */
+    uint32_t slot;               /* ring slot bytes (multiple of 16, >= 128 and >= every len) */
     size_t chunk, chunks;        /* frames per chunk, chunks in the ring (>= 2) */
     uint64_t total;              /* frames to push through */
     int producers, consumers;    /* threads per side (0: 1) */
     int digest;                  /* 1: sum a 64-bit digest of every transmitted frame + egress */
-    uint64_t *stats;             /* nullable: per-ifindex verdict counters, as hfv_br_process_host */
+    int inflight;                /* chunks on the GPU at once, each on its own stream (0: 2) */
+    int dma;                     /* 0: the kernel reads/writes the ring over PCIe (zero-copy);
+                                    1: each chunk is copied to HBM and back by the DMA engines */
+    uint64_t *stats;             /* nullable: per-ifindex verdict counters (added to), as hfv_br_process_host */
 };
 struct hfv_loop_stats {
     uint64_t rx_pkts, tx_pkts, tx_bytes, drop_pkts;
     uint64_t tx_digest;                         /* sum over transmitted frames (order-free) */
     uint64_t verdict_pkts[HFV_BR_COUNTERS];     /* frames per final verdict counter (verdict >> 3) */
     double seconds;                             /* wall time of the whole loop */
+    double gpu_busy_s, gpu_wait_s;              /* router stage: inside hfv_br_process_host / waiting for RX */
+    double producer_busy_s, consumer_busy_s;    /* summed over the threads of each side */
 };
 int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *cfg, struct hfv_loop_stats *out);
 

@@ -148,8 +148,8 @@ struct hfv_ctx {
     DevState *host_img = nullptr;         // pinned staging image
     hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
     DevState *dev_tab[2] = {nullptr, nullptr};
-    hipEvent_t tab_done[2] = {nullptr, nullptr};   // scratch events for the reader fence
     hipStream_t readers[2][8] = {};                // streams that launched with dev_tab[i]
+    hipEvent_t reader_ev[2][8] = {};               // recorded on readers[i][r] after each such launch
     int nreaders[2] = {0, 0};
     bool readers_overflow[2] = {false, false};
     int active = 0;
@@ -263,11 +263,11 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         if (ctx->readers_overflow[next]) {
             HIP_TRY(hipDeviceSynchronize());
         } else {
+            // the events were recorded after each reader's last launch with the table, so the
+            // fence holds even for a reader stream the caller has destroyed since
             for (int r = 0; r < ctx->nreaders[next]; ++r) {
-                hipStream_t rs = ctx->readers[next][r];
-                if (rs == st) continue;   // same stream: ordered already
-                HIP_TRY(hipEventRecord(ctx->tab_done[next], rs));
-                HIP_TRY(hipStreamWaitEvent(st, ctx->tab_done[next], 0));
+                if (ctx->readers[next][r] == st) continue;   // same stream: ordered already
+                HIP_TRY(hipStreamWaitEvent(st, ctx->reader_ev[next][r], 0));
             }
         }
         ctx->nreaders[next] = 0;
@@ -283,11 +283,17 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
 
 static void note_reader(hfv_ctx *ctx, hipStream_t st)
 {
-    int a = ctx->active;
-    for (int r = 0; r < ctx->nreaders[a]; ++r)
-        if (ctx->readers[a][r] == st) return;
-    if (ctx->nreaders[a] < 8) ctx->readers[a][ctx->nreaders[a]++] = st;
-    else ctx->readers_overflow[a] = true;
+    const int a = ctx->active;
+    int r = 0;
+    while (r < ctx->nreaders[a] && ctx->readers[a][r] != st) ++r;
+    if (r == ctx->nreaders[a]) {
+        if (r == 8) {
+            ctx->readers_overflow[a] = true;
+            return;
+        }
+        ctx->readers[a][ctx->nreaders[a]++] = st;
+    }
+    if (hipEventRecord(ctx->reader_ev[a][r], st) != hipSuccess) ctx->readers_overflow[a] = true;
 }
 
 static int after_launch(hfv_ctx *ctx, hipStream_t st, int err, const char *what)
@@ -326,7 +332,8 @@ int hfv_ctx_create(int device, hfv_ctx **out)
         for (int i = 0; i < 2; ++i) {
             if (hipMalloc((void **)&c->dev_tab[i], sizeof(DevState)) != hipSuccess) { rc = -ENOMEM; break; }
             if (hipMemset(c->dev_tab[i], 0, sizeof(DevState)) != hipSuccess) { rc = -EIO; break; }
-            if (hipEventCreateWithFlags(&c->tab_done[i], hipEventDisableTiming) != hipSuccess) { rc = -EIO; break; }
+            for (int r = 0; r < 8 && !rc; ++r)
+                if (hipEventCreateWithFlags(&c->reader_ev[i][r], hipEventDisableTiming) != hipSuccess) rc = -EIO;
         }
         if (rc) break;
         if (query_geometry(device, &c->geom) != 0) {
@@ -368,7 +375,8 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->h_bits[i]) (void)hipHostFree(ctx->h_bits[i]);
         if (ctx->d_rec[i]) (void)hipFree(ctx->d_rec[i]);
         if (ctx->d_bits[i]) (void)hipFree(ctx->d_bits[i]);
-        if (ctx->tab_done[i]) { (void)hipEventSynchronize(ctx->tab_done[i]); (void)hipEventDestroy(ctx->tab_done[i]); }
+        for (int r = 0; r < 8; ++r)
+            if (ctx->reader_ev[i][r]) (void)hipEventDestroy(ctx->reader_ev[i][r]);
         if (ctx->dev_tab[i]) (void)hipFree(ctx->dev_tab[i]);
     }
     for (int i = 0; i < 2; ++i) {
@@ -1102,6 +1110,53 @@ static int br_zero_copy(hfv_ctx *ctx, uint8_t *dframes, size_t slot, const uint1
     }
     return 0;
 }
+
+}  // extern "C"
+
+int hfv::br_zc_prepare(hfv_ctx *ctx)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    SVC_QUIESCE(ctx);
+    HIP_TRY(hipSetDevice(ctx->device));
+    return 0;
+}
+
+void hfv::forget_stream(hfv_ctx *ctx, void *stream)
+{
+    for (int a = 0; a < 2; ++a)
+        for (int r = 0; r < ctx->nreaders[a];)
+            if (ctx->readers[a][r] == (hipStream_t)stream) ctx->readers[a][r] = ctx->readers[a][--ctx->nreaders[a]];
+            else ++r;
+}
+
+int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen,
+                       const uint32_t *difx, size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats)
+{
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    int e = launch_br_process(ctx->geom, ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
+                              degr, dstats, st);
+    return after_launch(ctx, st, e, "br_process launch");
+}
+
+int hfv::br_zc_launch(hfv_ctx *ctx, void *stream, uint8_t *frames, size_t slot, const uint16_t *len,
+                      const uint32_t *ifx, size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress,
+                      uint64_t *dstats)
+{
+    if (n == 0) return 0;
+    uint8_t *df = host_dev_ptr(ctx, frames, n * slot);
+    uint16_t *dlen = (uint16_t *)host_dev_ptr(ctx, len, n * 2);
+    uint32_t *difx = (uint32_t *)host_dev_ptr(ctx, ifx, n * 4);
+    uint8_t *dact = host_dev_ptr(ctx, action, n), *dver = host_dev_ptr(ctx, verdict, n);
+    int32_t *degr = (int32_t *)host_dev_ptr(ctx, egress, n * 4);
+    if (!df || !dlen || !difx || !dact || !dver || !degr) return fail(-EINVAL, "zero-copy stage: buffer not registered");
+    return br_dev_launch(ctx, stream, df, slot, dlen, difx, n, dact, dver, degr, dstats);
+}
+
+extern "C" {
 
 int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,
                         const uint32_t *ingress_ifindex, size_t n, size_t window, uint8_t *action,

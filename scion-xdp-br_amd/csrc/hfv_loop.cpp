@@ -21,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "hfv_internal.h"
 
 namespace {
@@ -41,6 +43,18 @@ static uint64_t frame_hash(const uint8_t *p, size_t n, int32_t egress)
     memcpy(&w, p + i, n - i);
     h = (h ^ w) * 0x94D049BB133111EBull;
     return h ^ (h >> 31);
+}
+
+// Wait politely: spin briefly, then sleep in short steps (the box's CPU share is a quota; a
+// dozen threads spinning flat out get the whole process throttled).
+static void relax(unsigned &spins)
+{
+    if (++spins < 256) {
+        __builtin_ia32_pause();
+        return;
+    }
+    struct timespec ts = {0, 20000};
+    nanosleep(&ts, nullptr);
 }
 
 static double now_s()
@@ -76,9 +90,11 @@ static void pin(int numa_node)
     if (CPU_COUNT(&cpus) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus, &cpus);
 }
 
+// Ring slot of chunk k: state = 3k (free for chunk k), 3k + 1 (filled), 3k + 2 (processed); the
+// consumer of chunk k hands the slot to chunk k + chunks.  Tagging the state with the chunk
+// number keeps two producers (or consumers) whose chunks share a slot from both taking it.
 struct Chunk {
-    std::atomic<uint32_t> state{0};   // 0 free, 1 filled, 2 processed
-    uint64_t seq = 0;                 // first frame number in it
+    std::atomic<uint64_t> state{0};
     size_t n = 0;                     // frames in it
 };
 
@@ -89,8 +105,8 @@ using namespace hfv;
 extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struct hfv_loop_stats *out)
 {
     if (!ctx || !c || !out || !c->frames || !c->lens || c->n_frames == 0) return fail(-EINVAL, "null argument");
-    if (c->slot < 64 || (c->slot & 63) || c->chunk == 0 || c->chunks < 2 || c->total == 0)
-        return fail(-EINVAL, "slot must be a multiple of 64, chunk > 0, chunks >= 2, total > 0");
+    if (c->slot < 128 || (c->slot & 15) || c->chunk == 0 || c->chunks < 2 || c->total == 0)
+        return fail(-EINVAL, "slot must be a multiple of 16 and >= 128, chunk > 0, chunks >= 2, total > 0");
     for (size_t i = 0; i < c->n_frames; ++i)
         if (c->lens[i] > c->slot || c->lens[i] > c->frame_stride) return fail(-EINVAL, "frame %zu longer than its slot", i);
     memset(out, 0, sizeof *out);
@@ -106,10 +122,14 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         return fail(-ENOMEM, "ring allocation");
     }
     memset(meta, 0, meta_bytes);
-    uint16_t *len = (uint16_t *)meta;
-    uint32_t *ifx = (uint32_t *)(meta + nslots * 4);
-    int32_t *egr = (int32_t *)(meta + nslots * 8);
-    uint8_t *act = meta + nslots * 12, *ver = meta + nslots * 13;
+    // per-frame metadata, chunk by chunk: len u16 (in a 4 B/frame field) | ingress ifindex u32 |
+    // egress i32 | action u8 | verdict u8, so each chunk's inputs and outputs are one contiguous range each
+    const size_t C = c->chunk;
+    auto len_of = [&](size_t s) { return (uint16_t *)(meta + s * C * 16); };
+    auto ifx_of = [&](size_t s) { return (uint32_t *)(meta + s * C * 16 + C * 4); };
+    auto egr_of = [&](size_t s) { return (int32_t *)(meta + s * C * 16 + C * 8); };
+    auto act_of = [&](size_t s) { return meta + s * C * 16 + C * 12; };
+    auto ver_of = [&](size_t s) { return meta + s * C * 16 + C * 13; };
     int rc = hfv_host_register(ctx, ring, (nslots * c->slot + 4095) & ~(size_t)4095);
     if (!rc) {
         rc = hfv_host_register(ctx, meta, meta_bytes);
@@ -122,28 +142,33 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     }
     const int node = hfv_ctx_numa_node(ctx);
     std::vector<Chunk> ch(c->chunks);
+    for (size_t i = 0; i < c->chunks; ++i) ch[i].state.store(3 * i);
     const uint64_t nchunks_total = (c->total + c->chunk - 1) / c->chunk;
     std::atomic<bool> abort{false};
 
     // producers: chunk k by producer k % P (tcpreplay --loop of the frame list)
+    std::vector<double> busy(producers, 0.0);
     auto produce = [&](int p) {
         pin(node);
         for (uint64_t k = (uint64_t)p; k < nchunks_total && !abort.load(std::memory_order_relaxed); k += producers) {
             Chunk &cc = ch[k % c->chunks];
-            while (cc.state.load(std::memory_order_acquire) != 0)
+            for (unsigned spins = 0; cc.state.load(std::memory_order_acquire) != 3 * k; relax(spins))
                 if (abort.load(std::memory_order_relaxed)) return;
-            const size_t base = (k % c->chunks) * c->chunk;
-            const uint64_t first = k * c->chunk;
-            const size_t n = (size_t)(c->total - first < c->chunk ? c->total - first : c->chunk);
+            const double tb = now_s();
+            const size_t sl = k % c->chunks, base = sl * C;
+            uint16_t *len = len_of(sl);
+            uint32_t *ifx = ifx_of(sl);
+            const uint64_t first = k * C;
+            const size_t n = (size_t)(c->total - first < C ? c->total - first : C);
             for (size_t i = 0; i < n; ++i) {
                 const size_t f = (size_t)((first + i) % c->n_frames);
                 memcpy(ring + (base + i) * c->slot, c->frames + f * c->frame_stride, c->lens[f]);
-                len[base + i] = c->lens[f];
-                ifx[base + i] = c->rx_ifindex;
+                len[i] = c->lens[f];
+                ifx[i] = c->rx_ifindex;
             }
-            cc.seq = first;
             cc.n = n;
-            cc.state.store(1, std::memory_order_release);
+            busy[p] += now_s() - tb;
+            cc.state.store(3 * k + 1, std::memory_order_release);
         }
     };
     // consumers: transmit redirected frames (digest + byte count per egress), drop the rest
@@ -154,42 +179,115 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         memset(&s, 0, sizeof s);
         for (uint64_t k = (uint64_t)q; k < nchunks_total && !abort.load(std::memory_order_relaxed); k += consumers) {
             Chunk &cc = ch[k % c->chunks];
-            while (cc.state.load(std::memory_order_acquire) != 2)
+            for (unsigned spins = 0; cc.state.load(std::memory_order_acquire) != 3 * k + 2; relax(spins))
                 if (abort.load(std::memory_order_relaxed)) return;
-            const size_t base = (k % c->chunks) * c->chunk;
+            const double tb = now_s();
+            const size_t sl = k % c->chunks, base = sl * C;
+            const uint16_t *len = len_of(sl);
+            const int32_t *egr = egr_of(sl);
+            const uint8_t *act = act_of(sl), *ver = ver_of(sl);
             for (size_t i = 0; i < cc.n; ++i) {
-                const size_t j = base + i;
                 s.rx_pkts++;
-                if ((ver[j] >> 3) < HFV_BR_COUNTERS) s.verdict_pkts[ver[j] >> 3]++;   // enum verdict: counter << 3 | code
-                if (act[j] == 4) {   // XDP_REDIRECT to egr[j]
+                if ((ver[i] >> 3) < HFV_BR_COUNTERS) s.verdict_pkts[ver[i] >> 3]++;   // enum verdict: counter << 3 | code
+                if (act[i] == 4) {   // XDP_REDIRECT to egr[i]
                     s.tx_pkts++;
-                    s.tx_bytes += len[j];
-                    if (c->digest) s.tx_digest += frame_hash(ring + j * c->slot, len[j], egr[j]);
+                    s.tx_bytes += len[i];
+                    if (c->digest) s.tx_digest += frame_hash(ring + (base + i) * c->slot, len[i], egr[i]);
                 } else {
                     s.drop_pkts++;
                 }
             }
-            cc.state.store(0, std::memory_order_release);
+            s.consumer_busy_s += now_s() - tb;
+            cc.state.store(3 * (k + c->chunks), std::memory_order_release);
         }
     };
     std::vector<std::thread> th;
     const double t0 = now_s();
     for (int p = 0; p < producers; ++p) th.emplace_back(produce, p);
     for (int q = 0; q < consumers; ++q) th.emplace_back(consume, q);
-    // the GPU stage: the router over each filled chunk, in ring order
+    // the GPU stage: the router over each filled chunk, in ring order, `inflight` chunks at once
+    // on their own streams (a chunk is a few hundred microseconds of PCIe-bound kernel; the
+    // launch and completion wait of one overlap the others)
+    const int D = c->inflight > 0 ? (c->inflight < (int)c->chunks ? c->inflight : (int)c->chunks) : 2;
+    std::vector<hipStream_t> ss(D, nullptr);
+    std::vector<hipEvent_t> ev(D, nullptr);
+    uint64_t *dstats = nullptr;
+    const size_t stats_bytes = HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8;
+    if (!rc) rc = br_zc_prepare(ctx);
+    for (int i = 0; i < D && !rc; ++i) {
+        if (hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+            rc = fail(-EIO, "loop: stream/event creation failed");
+    }
+    std::vector<uint8_t *> dfr(D, nullptr), dmeta(D, nullptr);   // DMA variant: device twin per stream
+    for (int i = 0; i < D && !rc && c->dma; ++i)
+        if (hipMalloc((void **)&dfr[i], C * c->slot) != hipSuccess || hipMalloc((void **)&dmeta[i], C * 16) != hipSuccess)
+            rc = fail(-ENOMEM, "loop: device chunk buffers");
+    if (!rc && c->stats && (hipMalloc((void **)&dstats, stats_bytes) != hipSuccess ||
+                            hipMemset(dstats, 0, stats_bytes) != hipSuccess))
+        rc = fail(-ENOMEM, "loop: device counters");
+    double gpu_busy = 0, gpu_wait = 0;
+    uint64_t launched = 0, retired = 0;
+    // hand finished chunks to the consumers, in order: one (waiting for it) or all that are done
+    auto retire = [&](bool block) {
+        while (retired < launched) {
+            hipEvent_t e = ev[retired % D];
+            if (block) {
+                if (hipEventSynchronize(e) != hipSuccess) rc = fail(-EIO, "loop: router kernel failed");
+            } else if (hipEventQuery(e) != hipSuccess) {
+                return;
+            }
+            if (rc) return;
+            ch[retired % c->chunks].state.store(3 * retired + 2, std::memory_order_release);
+            ++retired;
+            if (block) return;
+        }
+    };
     for (uint64_t k = 0; k < nchunks_total && !rc; ++k) {
         Chunk &cc = ch[k % c->chunks];
-        while (cc.state.load(std::memory_order_acquire) != 1) {
+        const double tw = now_s();
+        for (unsigned spins = 0; cc.state.load(std::memory_order_acquire) != 3 * k + 1; relax(spins)) retire(false);
+        const double tb = now_s();
+        while (!rc && launched - retired >= (uint64_t)D) retire(true);   // its stream's previous chunk
+        if (rc) break;
+        const size_t sl = k % c->chunks;
+        uint8_t *fr = ring + sl * C * c->slot, *cm = meta + sl * C * 16;
+        const int q = (int)(k % D);
+        if (!c->dma) {
+            rc = br_zc_launch(ctx, ss[q], fr, c->slot, len_of(sl), ifx_of(sl), cc.n, act_of(sl), ver_of(sl),
+                              egr_of(sl), dstats);
+        } else {   // frames and inputs in by DMA, the router in HBM, frames and outputs back by DMA
+            uint8_t *m = dmeta[q];
+            if (hipMemcpyAsync(dfr[q], fr, cc.n * c->slot, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
+                hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess)
+                rc = fail(-EIO, "loop: H2D copy");
+            if (!rc)
+                rc = br_dev_launch(ctx, ss[q], dfr[q], c->slot, (uint16_t *)m, (uint32_t *)(m + C * 4), cc.n, m + C * 12,
+                                   m + C * 13, (int32_t *)(m + C * 8), dstats);
+            if (!rc && (hipMemcpyAsync(fr, dfr[q], cc.n * c->slot, hipMemcpyDeviceToHost, ss[q]) != hipSuccess ||
+                        hipMemcpyAsync(cm + C * 8, m + C * 8, C * 6, hipMemcpyDeviceToHost, ss[q]) != hipSuccess))
+                rc = fail(-EIO, "loop: D2H copy");
         }
-        const size_t base = (k % c->chunks) * c->chunk;
-        rc = hfv_br_process_host(ctx, ring + base * c->slot, c->slot, len + base, ifx + base, cc.n, 0, act + base,
-                                 ver + base, egr + base, c->stats);
-        cc.state.store(2, std::memory_order_release);
+        if (!rc && hipEventRecord(ev[q], ss[q]) != hipSuccess) rc = fail(-EIO, "loop: event record failed");
+        if (!rc) ++launched;
+        retire(false);
+        gpu_wait += tb - tw;
+        gpu_busy += now_s() - tb;
+    }
+    while (!rc && retired < launched) retire(true);
+    if (!rc && dstats) {
+        std::vector<uint64_t> tmp(stats_bytes / 8);
+        if (hipMemcpy(tmp.data(), dstats, stats_bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(-EIO, "loop: counters");
+        else
+            for (size_t i = 0; i < tmp.size(); ++i) c->stats[i] += tmp[i];
     }
     if (rc) abort.store(true);
     for (auto &t : th) t.join();
     const double t1 = now_s();
     out->seconds = t1 - t0;
+    out->gpu_busy_s = gpu_busy;
+    out->gpu_wait_s = gpu_wait;
+    for (int p = 0; p < producers; ++p) out->producer_busy_s += busy[p];
     for (int q = 0; q < consumers; ++q) {
         out->rx_pkts += part[q].rx_pkts;
         out->tx_pkts += part[q].tx_pkts;
@@ -197,6 +295,20 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         out->drop_pkts += part[q].drop_pkts;
         out->tx_digest += part[q].tx_digest;
         for (int v = 0; v < HFV_BR_COUNTERS; ++v) out->verdict_pkts[v] += part[q].verdict_pkts[v];
+        out->consumer_busy_s += part[q].consumer_busy_s;
+    }
+    for (int i = 0; i < D; ++i) {
+        if (ss[i]) {
+            (void)hipStreamSynchronize(ss[i]);
+            forget_stream(ctx, ss[i]);
+            (void)hipStreamDestroy(ss[i]);
+        }
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+    if (dstats) (void)hipFree(dstats);
+    for (int i = 0; i < D; ++i) {
+        if (dfr[i]) (void)hipFree(dfr[i]);
+        if (dmeta[i]) (void)hipFree(dmeta[i]);
     }
     hfv_host_unregister(ctx, meta);
     hfv_host_unregister(ctx, ring);

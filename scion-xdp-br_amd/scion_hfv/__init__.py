@@ -217,14 +217,16 @@ class LoopConfig(ctypes.Structure):
                 ("frame_stride", ctypes.c_size_t), ("rx_ifindex", ctypes.c_uint32), ("slot", ctypes.c_uint32),
                 ("chunk", ctypes.c_size_t), ("chunks", ctypes.c_size_t), ("total", ctypes.c_uint64),
                 ("producers", ctypes.c_int), ("consumers", ctypes.c_int), ("digest", ctypes.c_int),
-                ("stats", ctypes.c_void_p)]
+                ("inflight", ctypes.c_int), ("dma", ctypes.c_int), ("stats", ctypes.c_void_p)]
 
 
 class LoopStats(ctypes.Structure):
     """struct hfv_loop_stats"""
     _fields_ = [("rx_pkts", ctypes.c_uint64), ("tx_pkts", ctypes.c_uint64), ("tx_bytes", ctypes.c_uint64),
                 ("drop_pkts", ctypes.c_uint64), ("tx_digest", ctypes.c_uint64),
-                ("verdict_pkts", ctypes.c_uint64 * 11), ("seconds", ctypes.c_double)]
+                ("verdict_pkts", ctypes.c_uint64 * 11), ("seconds", ctypes.c_double),
+                ("gpu_busy_s", ctypes.c_double), ("gpu_wait_s", ctypes.c_double),
+                ("producer_busy_s", ctypes.c_double), ("consumer_busy_s", ctypes.c_double)]
 
 
 def loop_frame_digest(frame: bytes, egress: int) -> int:
@@ -364,7 +366,7 @@ class Ctx:
                                          _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats)))
 
     def loop_run(self, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
-                 consumers=2, digest=False, stats=None):
+                 consumers=2, digest=False, stats=None, inflight=2, dma=False):
         """Config 5 in one process (hfv_loop_run): `frames` (n x stride uint8) cycled into a
         registered RX ring, the router over each chunk, TX/drop consumers.  Returns a dict."""
         import numpy as np
@@ -373,11 +375,13 @@ class Ctx:
         cfg = LoopConfig(frames=frames.ctypes.data, lens=lens.ctypes.data, n_frames=frames.shape[0],
                          frame_stride=frames.shape[1], rx_ifindex=rx_ifindex, slot=slot, chunk=chunk,
                          chunks=chunks, total=total, producers=producers, consumers=consumers,
-                         digest=1 if digest else 0, stats=_ptr(stats))
+                         digest=1 if digest else 0, inflight=inflight, dma=1 if dma else 0, stats=_ptr(stats))
         st = LoopStats()
         _check(lib().hfv_loop_run(self._h, ctypes.byref(cfg), ctypes.byref(st)))
         return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,
-                "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds}
+                "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds,
+                "gpu_busy_s": st.gpu_busy_s, "gpu_wait_s": st.gpu_wait_s, "producer_busy_s": st.producer_busy_s,
+                "consumer_busy_s": st.consumer_busy_s}
 
     def host_register(self, buf):
         _check(lib().hfv_host_register(self._h, _ptr(buf), buf.nbytes))

@@ -42,14 +42,15 @@ def _oracle(frames, total, hf_check=True):
             "drop": int(reps[~tx].sum()), "tx_digest": digest, "verdicts": [int(x) for x in verdicts]}
 
 
+@pytest.mark.parametrize("dma", [False, True], ids=["zero_copy", "dma"])
 @pytest.mark.parametrize("hf_check", [True, False], ids=["hf_check", "hf_check_off"])
-def test_loop_matches_oracle(gpu_ctx, hf_check):
+def test_loop_matches_oracle(gpu_ctx, hf_check, dma):
     frames = _frame_mix(97, bad_every=5)
     E.setup_ctx(gpu_ctx, hf_check=hf_check)
     total = 10007
     stats = np.zeros((hfv.BR_STATS_IFINDEX, 2, hfv.BR_COUNTERS), dtype=np.uint64)
     got = gpu_ctx.loop_run(frames, np.full(97, E.FRAME_LEN), total, rx_ifindex=E.RX_IFINDEX, slot=SLOT,
-                           chunk=1000, chunks=3, producers=2, consumers=3, digest=True, stats=stats)
+                           chunk=1000, chunks=3, producers=2, consumers=3, digest=True, stats=stats, dma=dma)
     want = _oracle(frames, total, hf_check)
     for k in want:
         assert got[k] == want[k], k
@@ -59,19 +60,30 @@ def test_loop_matches_oracle(gpu_ctx, hf_check):
     assert int(stats[E.RX_IFINDEX, 0].sum()) == total * E.FRAME_LEN
 
 
+def test_loop_more_threads_than_ring_chunks(gpu_ctx):
+    """Producers and consumers outnumber the ring's chunks (chunks k and k + chunks share a slot
+    and belong to different threads), three chunks in flight on the GPU."""
+    frames = _frame_mix(31, bad_every=4)
+    E.setup_ctx(gpu_ctx)
+    got = gpu_ctx.loop_run(frames, np.full(31, E.FRAME_LEN), 20000, rx_ifindex=E.RX_IFINDEX, slot=144, chunk=500,
+                           chunks=3, producers=5, consumers=4, digest=True, inflight=3, dma=True)
+    want = _oracle(frames, 20000)
+    assert {k: got[k] for k in want} == want
+
+
 def test_loop_single_producer_ragged_tail(gpu_ctx):
     """One producer/consumer, total smaller than one chunk and not a multiple of n_frames."""
     frames = _frame_mix(7)
     E.setup_ctx(gpu_ctx)
     got = gpu_ctx.loop_run(frames, np.full(7, E.FRAME_LEN), 45, rx_ifindex=E.RX_IFINDEX, slot=SLOT, chunk=64,
-                           chunks=2, producers=1, consumers=1, digest=True)
+                           chunks=2, producers=1, consumers=1, digest=True, inflight=1)
     want = _oracle(frames, 45)
     assert {k: got[k] for k in want} == want
 
 
 def test_loop_rejects_bad_geometry(gpu_ctx):
     frames = _frame_mix(2)
-    for kw in ({"slot": 100}, {"slot": 128 - 64}, {"chunks": 1}, {"chunk": 0}):
+    for kw in ({"slot": 136}, {"slot": 112}, {"slot": 128}, {"chunks": 1}, {"chunk": 0}):
         args = dict(rx_ifindex=E.RX_IFINDEX, slot=SLOT, chunk=16, chunks=2)
         args.update(kw)
         with pytest.raises(hfv.HfvError):

@@ -323,3 +323,28 @@ def test_pinned_keymap_attach(ctx, tmp_path, monkeypatch):
     assert hfv.keymap_read(path)[0] == orc.hop_key(orc.KEY_1111)
     ctx.verify_records(d, n, bits)
     assert np.array_equal(bits_np(bits, n), g["pass_bits"])
+
+
+def test_table_update_after_reader_stream_destroyed(ctx):
+    """A key update after the stream that last read the key table was destroyed: the publish
+    fences on an event recorded after that stream's launch, never on the dead stream."""
+    import gc
+    raw = orc.KEY_1111
+    hk, valid = orc.key_table(raw)
+    ctx.key_add(0, raw)
+    recs = orc.gen_records(3000, hk, 0, seed=8)
+    want = orc.verify_records(recs, hk, valid, 0)
+    d = dev(recs)
+    for _ in range(3):
+        s = torch.cuda.Stream()
+        bits = new_bits(3000)
+        ctx.verify_records(d, 3000, bits, stream=s)
+        s.synchronize()
+        assert np.array_equal(bits_np(bits, 3000), want)
+        del s
+        gc.collect()
+        ctx.key_add(7, orc.KEY_1111)   # dirty: the next launch publishes a new table
+    bits = new_bits(3000)
+    ctx.verify_records(d, 3000, bits, stream=torch.cuda.Stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(bits_np(bits, 3000), want)

@@ -66,7 +66,7 @@ struct BrFrame {
     uint8_t *p;
     uint32_t row;      // dword index of this frame's staged header row in s_hdr
     int win;           // staged bytes (0: read and write everything in HBM)
-    bool dirty;        // the staged row was written (write it back at the end of the tile)
+    uint32_t dirty;    // 16-byte chunks of the staged row written (only those go back to HBM)
     int len;
     int lim;           // bytes of the frame present in the buffer (min(len, window))
     bool cut;          // a check failed only because the window ended before len
@@ -122,7 +122,7 @@ __device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
 {
     if (off < k.win) {
         reinterpret_cast<uint8_t *>(s_hdr + k.row)[off] = (uint8_t)v;
-        k.dirty = true;
+        k.dirty |= 1u << (off >> 4);
     } else {
         k.p[off] = (uint8_t)v;
     }
@@ -132,7 +132,7 @@ __device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
     if (off + 2 <= k.win) {   // whole field in the window (the common case): one check
         uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
-        k.dirty = true;
+        k.dirty |= (1u << (off >> 4)) | (1u << ((off + 1) >> 4));
     } else if (off >= k.win) {
         k.p[off] = (uint8_t)v; k.p[off + 1] = (uint8_t)(v >> 8);
     } else {
@@ -145,7 +145,7 @@ __device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
     if (off + 4 <= k.win) {
         uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
-        k.dirty = true;
+        k.dirty |= (1u << (off >> 4)) | (1u << ((off + 3) >> 4));
     } else if (off >= k.win) {
         uint8_t *q = k.p + off;
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
@@ -695,7 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         }
         const uint32_t len = pre_len, ifx = pre_ifx;
         uint64_t i = t * 64 + lane;
-        bool dirty = false;
+        uint32_t dirty = 0;
         if (i < n) {
             BrFrame k = {};
             k.p = pkts + i * slot;
@@ -708,8 +708,12 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             dirty = k.dirty;
         }
         if constexpr (WIN > 0) {
-            // write the rewritten rows back: 16-byte stores, WIN / 16 lanes per frame
-            uint64_t dmask = __ballot(dirty);
+            // write the rewritten 16-byte chunks back (WIN / 16 lanes per frame, each storing its
+            // chunk if the frame's lane wrote into it): untouched chunks stay clean in L2, so a
+            // frame whose changes lie in one 32-byte sector of a line costs that sector, not the line
+            uint32_t cmask[C];
+#pragma unroll
+            for (int r = 0; r < C; ++r) cmask[r] = (uint32_t)__shfl((int)dirty, r * (64 / C) + (int)fr_of);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
 #pragma unroll
             for (int r = 0; r < C; ++r) {
                 uint32_t fr = r * (64 / C) + fr_of;
-                if ((dmask >> fr) & 1u) {
+                if ((cmask[r] >> ch) & 1u) {
                     const uint32_t *q = rows + fr * kBrRow + 4 * ch;
                     *reinterpret_cast<uint4 *>(pkts + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
                 }

@@ -228,6 +228,38 @@ def test_full_size_properties(ctx, n):
     del recs
 
 
+@pytest.mark.parametrize("service", [False, True], ids=["launch", "service"])
+def test_full_size_properties_ifid(ctx, service):
+    """Config 3 at its BASELINE size (2^20 records, 256 ingress-interface keys, KEYSEL_IFID):
+    verdicts equal the generator's truth, an oracle-verified sample agrees, and the launch and
+    the resident-service paths give the same bitmap."""
+    n = 1 << 20
+    raw = orc.gen_key_table(256)
+    hk, valid = orc.key_table(raw)
+    install(ctx, raw)
+    ctx.set_keysel(1)
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=DEV)
+    ctx.gen_records(recs, n, orc.SEED_RECORDS)
+    bits = new_bits(n)
+    if service:
+        t = ctx.service_submit(recs, n, bits)
+        ctx.service_wait(t, 10000)
+        ctx.service_stop()
+    else:
+        ctx.verify_records(recs, n, bits)
+    torch.cuda.synchronize()
+    got = hfv.bits_to_bool(bits_np(bits, n), n)
+    assert np.array_equal(got, orc.expected_pass_rule(n))
+    idx = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
+    sample = recs[torch.from_numpy(idx).to(DEV)].cpu().numpy()
+    want = hfv.bits_to_bool(orc.verify_records(sample, hk, valid, 1), 4096)
+    assert np.array_equal(got[idx], want)
+    # the IFIDs really spread over the key table (not one slot)
+    ifids = np.where(sample[:, 40] & 1, sample[:, 51], sample[:, 53])   # Cons ? ConsIngress : ConsEgress (big-endian low byte)
+    assert len(np.unique(ifids)) > 200
+    del recs
+
+
 def test_host_path_matches_device(ctx):
     ctx.key_add(0, orc.KEY_1111)
     n = (1 << 21) + 777   # 8 full 2^18-record staging chunks and a ragged ninth

@@ -251,18 +251,17 @@ def ceilings(keysel, n, mhz, cus):
 
 
 def service_grid(ctx, batches, steps, bitmaps, n, posts=None):
-    """One resident-service grid over `steps` batches (batch k % R, bitmap k) posted by one
-    hfv_service_submitv call -- which launches the grid once they are in the ring -- and
-    stopped after the last; returns the grid's lifetime in ms.  posts: the prepared
-    descriptor array (built outside a timed region)."""
+    """One resident-service grid over `steps` batches (batch k % R, bitmap k): hfv_service_run
+    posts them and the stop behind them, launches the grid and waits for it; returns the
+    grid's lifetime in ms.  posts: the prepared descriptor array (built outside a timed
+    region)."""
     if posts is None:
         posts = ctx.service_batches([(batches[k % len(batches)], n, bitmaps[k % len(bitmaps)]) for k in range(steps)])
-    ctx.service_submitv(posts)
-    return ctx.service_stop()
+    return ctx.service_run(posts)[1]
 
 
 def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream, bitmap_cap=1024,
-               service=True):
+               service=True, reps=3):
     """Resident records in `rotate` batches, launch path and service path; returns a dict."""
     torch = W.torch
     R = rotate
@@ -315,10 +314,21 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     def service_run():
         svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
 
-    svc_el, per_rank = W.timed(1, service_run)
-    svc["mhz"] = ctx.service_shader_mhz()          # diagnostics, outside the timed region
-    check(steps)
-    out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": svc["grid_ms"], "mhz": svc["mhz"]})
+    # the K-step timed region is repeated `reps` times (each a fresh grid over the same K
+    # batches) and the median region is reported: one timed region of ~0.3 ms is exposed to a
+    # single host hiccup (one of three A/B runs measured 0.41 ms for a 0.245 ms grid)
+    runs = []
+    for _ in range(max(1, reps)):
+        for b in bitmaps:
+            b.zero_()
+        W.sync()
+        el, per_rank = W.timed(1, service_run)
+        runs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz()))   # clock: diagnostics, untimed
+        check(steps)
+    runs.sort(key=lambda r: r[0])
+    svc_el, per_rank, grid_ms, mhz = runs[len(runs) // 2]
+    out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
+                "svc_all_ms": [round(r[0] * 1e3, 4) for r in sorted(runs, key=lambda r: r[0])]})
     return out
 
 
@@ -721,7 +731,7 @@ def run_hf(args, W):
     ctx = make_ctx(hfv, W.device, keysel)
     stream = torch.cuda.current_stream().cuda_stream
     cus = torch.cuda.get_device_properties(W.device).multi_processor_count
-    m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream,
+    m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream, reps=args.svc_reps,
                    service=not args.launch_only)
     headline = "launch" if args.launch_only else args.mode
     elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
@@ -764,14 +774,16 @@ def run_hf(args, W):
                          note=f"step k verifies resident batch k % {args.rotate} ({args.rotate} x {n * 64 >> 20} MiB "
                               f"per GPU > 256 MiB Infinity Cache): records are read from HBM"),
         "ceilings": ceilings(args.keysel, n, m["mhz"], cus),
-        "path": ("resident service: one persistent grid; the K batches posted through the host descriptor ring "
-                 "by one hfv_service_submitv call, which launches the grid after them; posting, grid launch, table "
-                 "fill and drain inside the timed region"
+        "path": ("resident service: one persistent grid; the K batches and a stop descriptor posted through the "
+                 "host descriptor ring by one hfv_service_run call, which launches the grid after them and waits for "
+                 "it; posting, grid launch, table fill and drain inside the timed region"
                  if headline == "service" else "one hfv_verify_records launch per batch"),
         "service": None if args.launch_only else {
             "mpkts": round(total * args.steps / m["svc_el"] / 1e6, 2),
             "ms_per_step": round(m["svc_el"] / args.steps * 1e3, 5), "grid_ms": round(m["grid_ms"], 4),
-            "shader_mhz": round(m["mhz"], 1) if m["mhz"] else None},
+            "shader_mhz": round(m["mhz"], 1) if m["mhz"] else None,
+            "timed_regions_ms": m.get("svc_all_ms"),
+            "note": f"value = the median of {args.svc_reps} timed regions of K steps each (each a fresh grid)"},
         "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),
                        "ms_per_step": round(m["launch_el"] / args.steps * 1e3, 5),
                        "kernel_ms_mean": round(m["k_mean"], 5), "kernel_ms_median": round(m["k_med"], 5),
@@ -828,7 +840,8 @@ def run_hf(args, W):
     ref_bits = bits0.cpu().numpy().view(np.uint64).copy()
     if extras and keysel == hfv.KEYSEL_ZERO:   # config 3 beside the config-2 headline
         ctx3 = make_ctx(hfv, W.device, hfv.KEYSEL_IFID)
-        m3 = measure_hf(hfv, W, ctx3, "ifid", n, first, args.rotate, args.steps, args.warmup, stream)
+        m3 = measure_hf(hfv, W, ctx3, "ifid", n, first, args.rotate, args.steps, args.warmup, stream,
+                        reps=args.svc_reps)
         a3 = bytes_per_batch * args.steps / (m3["grid_ms"] * 1e-3) / 1e9
         result["config3"] = {"workload": f"config 3: {n} x 64 B records per GPU per step, 256 ingress-interface "
                                          "keys (KEYSEL_IFID), same rotation and timing as the headline",
@@ -904,6 +917,7 @@ def main():
     ap.add_argument("--loop-dma", action="store_true", help="config-5 loop: chunks through HBM by DMA, not zero-copy")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
+    ap.add_argument("--svc-reps", type=int, default=3, help="timed service regions of K steps (median reported)")
     ap.add_argument("--launch-only", action="store_true",
                     help="measure the launch path only (ranks sharing one GPU cannot each hold a service grid)")
     ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")

@@ -184,6 +184,12 @@ struct hfv_batch {
     uint64_t *pass_bits;
 };
 int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket);
+/* One-shot run: the batches on a fresh grid (a running service is stopped first), with the
+ * stop descriptor posted right behind them, so the grid exits as soon as the last batch is
+ * verified; returns when it has (every ticket done) with the grid's lifetime in *kernel_ms
+ * (nullable).  For a known set of batches it saves posting and relaying a stop afterwards. */
+int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
+                    float *kernel_ms);
 /* Tickets are monotonic over the ctx's life, across service restarts (key changes, idle
  * exits): a ticket of a stopped grid reports done, or -EIO if that grid exited on its idle
  * timeout without verifying it. */

@@ -202,6 +202,7 @@ struct hfv_ctx {
     uint64_t svc_ticket = 1;         // next ticket
     std::vector<uint64_t> svc_lost;  // tickets of stopped grids that were never verified (bounded)
     uint64_t svc_tag = 0;            // generation of the running grid << 40 (see s_svc_tag)
+    bool svc_stop_posted = false;    // the running grid's stop descriptor is already in the ring
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
 };
 
@@ -1432,9 +1433,9 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
 {
     if (kernel_ms) *kernel_ms = 0.0f;
     if (!ctx->svc_running) return 0;
-    const uint64_t last = ctx->svc_next - 1;   // last batch posted
+    const uint64_t last = ctx->svc_next - 1 - (ctx->svc_stop_posted ? 1 : 0);   // last batch posted
     int rc = 0;
-    if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0)
+    if (!ctx->svc_stop_posted && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0)
         rc = svc_post(ctx, 0, 0, kSvcStopN, 0, nullptr);
     // the grid exits on the stop descriptor, or on its idle timeout if the post failed.  Spin
     // on the stream for a while first: the blocking wait sleeps on an interrupt, whose wake-up
@@ -1527,6 +1528,7 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
     ctx->svc_idle_ms = idle_ms ? idle_ms : 1000;
     ctx->svc_next = 1;
     ctx->svc_base = ctx->svc_ticket;
+    ctx->svc_stop_posted = false;
     return 0;
 }
 
@@ -1628,6 +1630,54 @@ int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t co
         if (i == 0) *first_ticket = t;
     }
     return launch ? svc_launch(ctx, launch) : 0;
+}
+
+int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
+                    float *kernel_ms)
+{
+    if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
+    *first_ticket = 0;
+    if (kernel_ms) *kernel_ms = 0.0f;
+    for (size_t i = 0; i < count; ++i) {
+        int rc = svc_check_batch(ctx, batches[i].recs, batches[i].stride, batches[i].n, batches[i].pass_bits);
+        if (rc) {
+            char why[256];
+            snprintf(why, sizeof why, "%s", hfv_last_error());
+            return fail(rc, "batch %zu: %s", i, why);
+        }
+    }
+    DeviceGuard g(ctx->device);
+    int rc = svc_quiesce(ctx);
+    if (rc) return rc;
+    DevState *ds;
+    rc = svc_begin(ctx, ctx->svc_idle_ms, &ds);
+    if (rc) return rc;
+    // the batches, then the stop right behind them, are in the ring before the grid starts (a
+    // longer run launches once the ring is full): the grid exits as soon as its blocks finish
+    // their share of the last batch, with no stop to post and relay afterwards
+    bool launched = false;
+    for (size_t i = 0; i <= count && !rc; ++i) {
+        if (!launched && ctx->svc_next > (uint64_t)kSvcRing) {
+            rc = svc_launch(ctx, ds);
+            launched = true;
+            if (rc) break;
+        }
+        if (i == count) {
+            rc = svc_post(ctx, 0, 0, kSvcStopN, 0, nullptr);
+            ctx->svc_stop_posted = rc == 0;
+            break;
+        }
+        uint64_t t = 0;
+        rc = svc_post(ctx, (uint64_t)(uintptr_t)batches[i].recs, (uint64_t)(uintptr_t)batches[i].pass_bits,
+                      batches[i].n, batches[i].stride, &t);
+        if (i == 0) *first_ticket = t;
+    }
+    if (!launched) {
+        int lr = svc_launch(ctx, ds);
+        if (lr) return lr;
+    }
+    int sr = svc_stop(ctx, kernel_ms);
+    return rc ? rc : sr;
 }
 
 int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)

@@ -98,6 +98,7 @@ def lib():
         "hfv_service_start": (i32, [vp, u32]),
         "hfv_service_submit": (i32, [vp, vp, sz, sz, vp, ctypes.POINTER(u64)]),
         "hfv_service_submitv": (i32, [vp, vp, sz, ctypes.POINTER(u64)]),
+        "hfv_service_run": (i32, [vp, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
         "hfv_service_poll": (i32, [vp, u64]),
         "hfv_service_wait": (i32, [vp, u64, i32]),
         "hfv_service_stop": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
@@ -439,6 +440,15 @@ class Ctx:
         t = ctypes.c_uint64()
         _check(lib().hfv_service_submitv(self._h, arr, len(arr), ctypes.byref(t)))
         return list(range(t.value, t.value + len(arr)))
+
+    def service_run(self, batches):
+        """One-shot: the batches on a fresh grid with the stop posted behind them; returns
+        (tickets, grid lifetime in ms) once every batch is verified (hfv_service_run)."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        t = ctypes.c_uint64()
+        ms = ctypes.c_float(0.0)
+        _check(lib().hfv_service_run(self._h, arr, len(arr), ctypes.byref(t), ctypes.byref(ms)))
+        return list(range(t.value, t.value + len(arr))), ms.value
 
     def service_poll(self, ticket):
         rc = lib().hfv_service_poll(self._h, ticket)

@@ -199,6 +199,33 @@ def test_service_submitv_golden_ifid(ctx):
         assert np.array_equal(bits_np(o, b - a), orc.verify_records(g["records"][a:b], hk, valid, 1))
 
 
+@pytest.mark.parametrize("count", [1, 5, 300], ids=["one", "five", "past_ring"])
+def test_service_run_one_shot(ctx, count):
+    """hfv_service_run: batches + stop posted before the grid starts (a run longer than the
+    ring launches once it is full); every ticket is done on return, bitmaps equal the
+    oracle's, and the ctx serves a later submit on a new grid."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    torch.cuda.synchronize()
+    cuts = [(k * 7) % (n - 64) for k in range(count)]
+    outs = [new_bits(n - c, fill=-1) for c in cuts]
+    ts, ms = ctx.service_run([(d[c:], n - c, o) for c, o in zip(cuts, outs)])
+    assert len(ts) == count and ms > 0 and not ctx.service_running
+    for t in ts:
+        assert ctx.service_poll(t)
+    hk, valid = orc.key_table(orc.KEY_1111)
+    for c, o in zip(cuts, outs):
+        assert np.array_equal(bits_np(o, n - c), orc.verify_records(g["records"][c:], hk, valid, 0))
+    bits = new_bits(n, fill=-1)
+    t = ctx.service_submit(d, n, bits)
+    ctx.service_wait(t, 20000)
+    assert np.array_equal(bits_np(bits, n), g["pass_bits"])
+    assert ts[-1] < t
+    ctx.service_stop()
+
+
 def test_service_no_key_fails_closed(ctx):
     g = orc.load_golden("hf_single.npz")
     n = len(g["records"])

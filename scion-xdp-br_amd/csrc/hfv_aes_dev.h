@@ -19,20 +19,6 @@ static __constant__ uint32_t c_t0[256] = {T0V64(0), T0V64(64), T0V64(128), T0V64
 #undef T0V8
 #undef T0V
 
-// HFV_GT3 = 1 (experiment, default off): the four-table rounds take their T3 lookups from
-// this compact 1 KiB global table through the vector L1 instead of LDS, so ~24 % of the
-// lookups run on the vector-memory path beside ds_read (scripts/ubench/tcp_gather.hip).
-#ifndef HFV_GT3
-#define HFV_GT3 0
-#endif
-#define T3V(i) rotl32(kTables.t0[i], 24)
-#define T3V8(i) T3V(i), T3V(i + 1), T3V(i + 2), T3V(i + 3), T3V(i + 4), T3V(i + 5), T3V(i + 6), T3V(i + 7)
-#define T3V64(i) T3V8(i), T3V8(i + 8), T3V8(i + 16), T3V8(i + 24), T3V8(i + 32), T3V8(i + 40), T3V8(i + 48), T3V8(i + 56)
-static __constant__ uint32_t c_t3[256] = {T3V64(0), T3V64(64), T3V64(128), T3V64(192)};
-#undef T3V64
-#undef T3V8
-#undef T3V
-__device__ __forceinline__ uint32_t glu3(uint32_t w) { return c_t3[w >> 24]; }
 
 // Round tables in LDS.  Layout (byte address of table t at index x for lane L):
 //   (x << 8) | ((t & 1) << 7) | ((L & 31) << 2) | ((t >> 1) << 16)

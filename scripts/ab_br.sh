@@ -1,14 +1,10 @@
 #!/bin/bash
-# A/B of router-kernel builds on one box: bench.py --workload br with each library in
-# scion-xdp-br_amd/lib/ab/ (HFV_LIB override), two interleaved rounds.
+# Interleaved A/B of library builds on the config-4 kernel:  scripts/ab_br.sh ROUNDS lib1.so lib2.so ...
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-for round in 1 2; do
-  for so in scion-xdp-br_amd/lib/ab/*.so; do
-    tag=$(basename $so .so)
-    echo "=== $round $tag"
-    HFV_LIB=$PWD/$so timeout -k 10 180 python bench.py --workload br --cpu-budget 0 --steps 5 > gpurun_out/ab_${tag}_$round.log 2>&1 || exit $?
-    python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['roofline']['kernel_ms_mean'], d['value'])" gpurun_out/ab_${tag}_$round.log
+R=$1; shift
+for r in $(seq 1 $R); do
+  for lib in "$@"; do
+    out=$(HFV_LIB=$(readlink -f $lib) timeout -k 10 200 python3 bench.py --workload br --steps 10 --warmup 3 --cpu-budget 0 2>/dev/null | grep '^{') || { echo "$lib failed"; exit 1; }
+    echo "$r $(basename $lib) $(echo "$out" | python3 -c 'import json,sys; d=json.load(sys.stdin); r=d["roofline"]; print("kernel_ms", r["kernel_ms_mean"], "median", r["kernel_ms_median"], "value", d["value"])')"
   done
 done

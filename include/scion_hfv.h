@@ -127,6 +127,13 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path);
  * recs: n records of `stride` bytes (8-byte aligned, stride % 8 == 0). */
 int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                        void *stream);
+/* record_verdict (xdp.c:54-70) for the verify-only paths: counters[slot][0] += packets that
+ * verified, counters[slot][1] += packets dropped as VERDICT_INVALID_HF, where slot is the
+ * packet's AS-ingress interface (IFID & 0xff, Cons ? HF.ingress : HF.egress, xdp.c:151-157),
+ * from the records and the verdict bitmap hfv_verify_records or the service wrote for them.
+ * counters: device u64[256][2], added to.  Stream-ordered like hfv_verify_records. */
+int hfv_verdict_counters(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, const uint64_t *pass_bits,
+                         uint64_t *counters, void *stream);
 /* verify_hop_field (xdp.c:77-91) for n prepared inputs: macinput[i] against the 48-bit
  * expected[i] (low 48 bits of the LE u64, as defer_verify_hop_field stores it).
  * key_index: per-packet slot (device u8 array) or NULL for slot 0. */

@@ -689,6 +689,24 @@ int hfv_gen_records(hfv_ctx *ctx, void *recs, size_t stride, size_t n, uint64_t 
     return after_launch(ctx, st, e, "gen_records launch");
 }
 
+int hfv_verdict_counters(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, const uint64_t *pass_bits,
+                         uint64_t *counters, void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!recs || !pass_bits || !counters) return fail(-EINVAL, "null buffer");
+    if (stride < (size_t)ctx->inf_off + 8 || stride < (size_t)ctx->hf_off + 12)
+        return fail(-EINVAL, "stride %zu too small for INF@%u/HF@%u", stride, ctx->inf_off, ctx->hf_off);
+    if (((uintptr_t)pass_bits & 7) || ((uintptr_t)counters & 7)) return fail(-EINVAL, "bitmap and counters must be 8-byte aligned");
+    DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
+    hipStream_t st = pick_stream(ctx, stream);
+    int e = launch_count_verdicts(ctx->geom, (const uint8_t *)recs, stride, n, ctx->inf_off, ctx->hf_off, pass_bits,
+                                  counters, st);
+    if (e != hipSuccess) return hip_fail((hipError_t)e, "count_verdicts launch");
+    return 0;
+}
+
 // ---- full border-router path (config 4) ---------------------------------------------------
 
 int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)

@@ -139,6 +139,8 @@ int launch_cmac_tags(const LaunchGeom &g, const DevKeyTable *tab, const void *mi
                      void *tags, void *stream);
 int launch_expand_keys(const uint8_t *raw, size_t n, hop_key *out, DevKeyTable *tab, uint32_t first_slot,
                        void *stream);
+int launch_count_verdicts(const LaunchGeom &g, const uint8_t *recs, size_t stride, size_t n, uint32_t inf_off,
+                          uint32_t hf_off, const uint64_t *bits, uint64_t *counters, void *stream);
 int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
                        size_t n, uint64_t seed, uint64_t first_index, void *stream);
 int query_geometry(int device, LaunchGeom *g);

@@ -1401,6 +1401,43 @@ int launch_expand_keys(const uint8_t *raw, size_t n, hop_key *out, DevKeyTable *
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// record_verdict for the verify-only paths (xdp.c:54-70): per AS-ingress interface (the
+// KEYSEL_IFID slot, IFID & 0xff, xdp.c:151-157) the packets that verified and the packets
+// dropped as VERDICT_INVALID_HF, from the records and a verdict bitmap of either verify path.
+// One lane per record; a block histogram in LDS, added to the u64 counters with one global
+// atomic per non-zero bin.  HBM-bound: the three bytes it reads lie in the record's 64-byte line.
+// ---------------------------------------------------------------------------------------
+constexpr int kCountBlock = 512;
+__global__ __launch_bounds__(kCountBlock) void k_count_verdicts(const uint8_t *__restrict__ recs, uint64_t stride,
+                                                                uint64_t n, uint32_t inf_off, uint32_t hf_off,
+                                                                const uint64_t *__restrict__ bits,
+                                                                unsigned long long *__restrict__ counters)
+{
+    __shared__ uint32_t h[512];
+    for (uint32_t i = threadIdx.x; i < 512; i += kCountBlock) h[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kCountBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kCountBlock) {
+        const uint8_t *r = recs + i * stride;
+        // Cons ? ConsIngress : ConsEgress, low byte of the big-endian field (rec_key_slot)
+        const uint32_t slot = (r[inf_off] & 1u) ? r[hf_off + 3] : r[hf_off + 5];
+        const uint32_t pass = (uint32_t)(bits[i >> 6] >> (i & 63)) & 1u;
+        atomicAdd(&h[slot * 2 + (pass ^ 1u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 512; i += kCountBlock)
+        if (h[i]) atomicAdd(counters + i, (unsigned long long)h[i]);
+}
+
+int launch_count_verdicts(const LaunchGeom &g, const uint8_t *recs, size_t stride, size_t n, uint32_t inf_off,
+                          uint32_t hf_off, const uint64_t *bits, uint64_t *counters, void *stream)
+{
+    unsigned grid = grid_for(n, kCountBlock, g.num_cus, 1);
+    hipLaunchKernelGGL(k_count_verdicts, dim3(grid), dim3(kCountBlock), 0, (hipStream_t)stream, recs, (uint64_t)stride,
+                       (uint64_t)n, inf_off, hf_off, bits, (unsigned long long *)counters);
+    return (int)hipGetLastError();
+}
+
 int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
                        size_t n, uint64_t seed, uint64_t first_index, void *stream)
 {

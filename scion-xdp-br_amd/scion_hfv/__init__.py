@@ -75,6 +75,7 @@ def lib():
         "hfv_keymap_erase": (i32, [ctypes.c_char_p, u32]),
         "hfv_keymap_read": (i32, [ctypes.c_char_p, vp, vp]),
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+        "hfv_verdict_counters": (i32, [vp, vp, sz, sz, vp, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
         "hfv_br_set_hf_check": (i32, [vp, i32]),
         "hfv_br_config_load": (i32, [ctypes.c_char_p, vp, sz, vp, sz, vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
@@ -335,6 +336,12 @@ class Ctx:
         _check(lib().hfv_verify_records_timed(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _stream(stream),
                                               ctypes.byref(ms)))
         return ms.value
+
+    def verdict_counters(self, recs, n, pass_bits, counters, stride=REC_SIZE, stream=None):
+        """record_verdict for the verify-only paths: counters (device u64[256][2]) +=
+        [verified, INVALID_HF] per AS-ingress IFID & 0xff (hfv_verdict_counters)."""
+        _check(lib().hfv_verdict_counters(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _ptr(counters),
+                                          _stream(stream)))
 
     def describe(self):
         buf = ctypes.create_string_buffer(256)

@@ -380,3 +380,37 @@ def test_table_update_after_reader_stream_destroyed(ctx):
     ctx.verify_records(d, 3000, bits, stream=torch.cuda.Stream())
     torch.cuda.synchronize()
     assert np.array_equal(bits_np(bits, 3000), want)
+
+
+@pytest.mark.parametrize("keysel", [0, 1])
+def test_verdict_counters(ctx, keysel):
+    """record_verdict for the verify-only paths: per AS-ingress IFID & 0xff, verified and
+    INVALID_HF packets, from records + bitmap of the launch path and of the service; equal to
+    the counts derived from the oracle's verdicts; counters are added to."""
+    rng = np.random.default_rng(21 + keysel)
+    raw = orc.gen_key_table(256)
+    hk, valid = orc.key_table(raw)
+    install(ctx, raw)
+    ctx.set_keysel(keysel)
+    recs = orc.gen_records(30011, hk, keysel, seed=123)
+    junk = rng.random(len(recs)) < 0.1
+    recs[junk] = rng.integers(0, 256, size=(int(junk.sum()), 64), dtype=np.uint8)
+    n = len(recs)
+    want_bits = orc.verify_records(recs, hk, valid, keysel)
+    passed = hfv.bits_to_bool(want_bits, n)
+    slot = np.where(recs[:, 40] & 1, recs[:, 51], recs[:, 53]).astype(np.int64)
+    want = np.zeros((256, 2), dtype=np.uint64)
+    np.add.at(want, (slot, (~passed).astype(np.int64)), 1)
+    d = dev(recs)
+    bits = new_bits(n)
+    ctx.verify_records(d, n, bits)
+    counters = torch.zeros((256, 2), dtype=torch.int64, device=DEV)
+    ctx.verdict_counters(d, n, bits, counters)
+    assert np.array_equal(host(counters).view(np.uint64), want)
+    # the service's bitmap, counted into the same (added-to) counters
+    sbits = new_bits(n)
+    t = ctx.service_submit(d, n, sbits)
+    ctx.service_wait(t, 20000)
+    ctx.verdict_counters(d, n, sbits, counters)
+    assert np.array_equal(host(counters).view(np.uint64), 2 * want)
+    assert int(want[:, 1].sum()) == int((~passed).sum()) and int(want.sum()) == n

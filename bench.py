@@ -653,7 +653,7 @@ def host_leg(hfv, W, ctx, recs, n, ref_bits):
                                            "whole 64 B lines), bitmap written to registered host memory"}}
 
 
-def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=192, inflight=3, dma=False):
+def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, inflight=3, dma=False):
     """Config 5 in one process (hfv_loop_run): gen_packets.py's 1000 frames cycled by producer
     threads into a registered RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each
     chunk zero-copy, consumer threads counting transmitted frames and dropping the rest."""
@@ -679,9 +679,10 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=192, i
                                 "router_waiting_for_rx": round(r["gpu_wait_s"] / r["seconds"], 3),
                                 "producer": round(r["producer_busy_s"] / producers / r["seconds"], 3),
                                 "consumer": round(r["consumer_busy_s"] / consumers / r["seconds"], 3)},
-            "path": "producer threads memcpy 138 B frames into a registered host RX ring (192 B slots) -> "
-                    "hfv_br_process_host zero-copy per chunk (kernel reads headers over PCIe, writes rewritten "
-                    "rows back) -> consumer threads count TX / drop; producers and consumers on the GPU's NUMA node",
+            "path": f"producer threads memcpy 138 B frames into a pinned, mapped host RX ring ({slot} B slots) -> "
+                    "the router kernel per chunk (zero-copy: reads headers over PCIe, writes rewritten rows back; or "
+                    "DMA through HBM) -> consumer threads count TX / drop; producers and consumers on the GPU's NUMA "
+                    "node",
             "veth": "not used: the GPU box runs commands as an unprivileged user with user namespaces disabled "
                     "(unshare -Urn: ENOSPC) and no CAP_NET_RAW (AF_PACKET: EPERM), so no veth pair can be made "
                     "there (scripts/netns_gpu_probe.py, DESIGN.md)"}
@@ -912,7 +913,7 @@ def main():
     ap.add_argument("--loop-chunks", type=int, default=12, help="config-5 loop ring chunks")
     ap.add_argument("--loop-threads", type=int, default=4, help="config-5 loop producer threads")
     ap.add_argument("--loop-consumers", type=int, default=2, help="config-5 loop consumer threads")
-    ap.add_argument("--loop-slot", type=int, default=192, help="config-5 loop ring slot bytes")
+    ap.add_argument("--loop-slot", type=int, default=144, help="config-5 loop ring slot bytes")
     ap.add_argument("--loop-inflight", type=int, default=3, help="config-5 loop chunks on the GPU at once")
     ap.add_argument("--loop-dma", action="store_true", help="config-5 loop: chunks through HBM by DMA, not zero-copy")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",

@@ -1161,20 +1161,6 @@ int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot
     return after_launch(ctx, st, e, "br_process launch");
 }
 
-int hfv::br_zc_launch(hfv_ctx *ctx, void *stream, uint8_t *frames, size_t slot, const uint16_t *len,
-                      const uint32_t *ifx, size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress,
-                      uint64_t *dstats)
-{
-    if (n == 0) return 0;
-    uint8_t *df = host_dev_ptr(ctx, frames, n * slot);
-    uint16_t *dlen = (uint16_t *)host_dev_ptr(ctx, len, n * 2);
-    uint32_t *difx = (uint32_t *)host_dev_ptr(ctx, ifx, n * 4);
-    uint8_t *dact = host_dev_ptr(ctx, action, n), *dver = host_dev_ptr(ctx, verdict, n);
-    int32_t *degr = (int32_t *)host_dev_ptr(ctx, egress, n * 4);
-    if (!df || !dlen || !difx || !dact || !dver || !degr) return fail(-EINVAL, "zero-copy stage: buffer not registered");
-    return br_dev_launch(ctx, stream, df, slot, dlen, difx, n, dact, dver, degr, dstats);
-}
-
 extern "C" {
 
 int hfv_br_process_host(hfv_ctx *ctx, uint8_t *frames, size_t slot, const uint16_t *len,

@@ -174,14 +174,12 @@ void keymap_close(const void *mapping);
 uint32_t keymap_seq(const void *mapping);
 uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8]);
 
-// Zero-copy router stage for in-library pipelines (hfv_loop.cpp): br_zc_prepare stops a running
-// service and makes the ctx's device current; br_zc_launch enqueues hfv_br_process over frames
-// and metadata that all lie in registered host buffers on `stream` (any stream of the ctx's
-// device) without waiting, adding the verdict counters to the device array dstats (nullable).
+// Router stage for in-library pipelines (hfv_loop.cpp): br_zc_prepare stops a running service
+// and makes the ctx's device current; br_dev_launch enqueues hfv_br_process on `stream` (any
+// stream of the ctx's device) without waiting, over device-addressable frames and metadata
+// (HBM, or the device view of mapped host memory), adding the verdict counters to the device
+// array dstats (nullable).
 int br_zc_prepare(hfv_ctx *ctx);
-int br_zc_launch(hfv_ctx *ctx, void *stream, uint8_t *frames, size_t slot, const uint16_t *len, const uint32_t *ifx,
-                 size_t n, uint8_t *action, uint8_t *verdict, int32_t *egress, uint64_t *dstats);
-// The same over device buffers (the DMA variant of the pipeline copies chunks in and out itself).
 int br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen, const uint32_t *difx,
                   size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats);
 // Before destroying a stream that launched with the ctx's tables (after synchronizing it):

@@ -1,7 +1,7 @@
 // hfv_loop.cpp -- config 5's end-to-end loop in one process: an RX ring in host memory fed by
 // producer threads (the NIC / veth side: tcpreplay of gen_packets.py's frames,
 // br/evaluation/gen_packets.py:41-71, README.md:131-139), the border router on the GPU
-// (hfv_br_process_host, zero-copy: the kernel reads the header windows of the registered ring
+// (the router kernel zero-copy: it reads the header windows of the pinned, mapped ring
 // over PCIe and writes the rewritten rows back), and consumer threads on the TX side that
 // transmit redirected frames and drop the rest while counting them (count_and_drop.py).
 //
@@ -112,14 +112,20 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     memset(out, 0, sizeof *out);
     const size_t nslots = c->chunk * c->chunks;
     const int producers = c->producers > 0 ? c->producers : 1, consumers = c->consumers > 0 ? c->consumers : 1;
-    // the RX ring and the per-frame metadata, registered so the kernel reads and writes them in place
-    uint8_t *ring = (uint8_t *)aligned_alloc(4096, (nslots * c->slot + 4095) & ~(size_t)4095);
+    // the RX ring and the per-frame metadata in pinned, mapped host memory: the kernel reads
+    // and writes them in place (zero-copy), or the DMA engines copy them (dma = 1)
+    int rc = br_zc_prepare(ctx);   // stops a running service; the ctx's device is current
+    if (rc) return rc;
+    const size_t ring_bytes = (nslots * c->slot + 4095) & ~(size_t)4095;
     const size_t meta_bytes = (nslots * 16 + 4095) & ~(size_t)4095;
-    uint8_t *meta = (uint8_t *)aligned_alloc(4096, meta_bytes);
-    if (!ring || !meta) {
-        free(ring);
-        free(meta);
-        return fail(-ENOMEM, "ring allocation");
+    uint8_t *ring = nullptr, *meta = nullptr, *dring = nullptr, *dmeta = nullptr;
+    if (hipHostMalloc((void **)&ring, ring_bytes, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void **)&meta, meta_bytes, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&dring, ring, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&dmeta, meta, 0) != hipSuccess) {
+        if (ring) (void)hipHostFree(ring);
+        if (meta) (void)hipHostFree(meta);
+        return fail(-ENOMEM, "loop: pinned ring allocation");
     }
     memset(meta, 0, meta_bytes);
     // per-frame metadata, chunk by chunk: len u16 (in a 4 B/frame field) | ingress ifindex u32 |
@@ -130,16 +136,6 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     auto egr_of = [&](size_t s) { return (int32_t *)(meta + s * C * 16 + C * 8); };
     auto act_of = [&](size_t s) { return meta + s * C * 16 + C * 12; };
     auto ver_of = [&](size_t s) { return meta + s * C * 16 + C * 13; };
-    int rc = hfv_host_register(ctx, ring, (nslots * c->slot + 4095) & ~(size_t)4095);
-    if (!rc) {
-        rc = hfv_host_register(ctx, meta, meta_bytes);
-        if (rc) hfv_host_unregister(ctx, ring);
-    }
-    if (rc) {
-        free(ring);
-        free(meta);
-        return rc;
-    }
     const int node = hfv_ctx_numa_node(ctx);
     std::vector<Chunk> ch(c->chunks);
     for (size_t i = 0; i < c->chunks; ++i) ch[i].state.store(3 * i);
@@ -213,15 +209,14 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     std::vector<hipEvent_t> ev(D, nullptr);
     uint64_t *dstats = nullptr;
     const size_t stats_bytes = HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8;
-    if (!rc) rc = br_zc_prepare(ctx);
     for (int i = 0; i < D && !rc; ++i) {
         if (hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
             rc = fail(-EIO, "loop: stream/event creation failed");
     }
-    std::vector<uint8_t *> dfr(D, nullptr), dmeta(D, nullptr);   // DMA variant: device twin per stream
+    std::vector<uint8_t *> dfr(D, nullptr), dmt(D, nullptr);   // DMA variant: device twin per stream
     for (int i = 0; i < D && !rc && c->dma; ++i)
-        if (hipMalloc((void **)&dfr[i], C * c->slot) != hipSuccess || hipMalloc((void **)&dmeta[i], C * 16) != hipSuccess)
+        if (hipMalloc((void **)&dfr[i], C * c->slot) != hipSuccess || hipMalloc((void **)&dmt[i], C * 16) != hipSuccess)
             rc = fail(-ENOMEM, "loop: device chunk buffers");
     if (!rc && c->stats && (hipMalloc((void **)&dstats, stats_bytes) != hipSuccess ||
                             hipMemset(dstats, 0, stats_bytes) != hipSuccess))
@@ -253,11 +248,12 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         const size_t sl = k % c->chunks;
         uint8_t *fr = ring + sl * C * c->slot, *cm = meta + sl * C * 16;
         const int q = (int)(k % D);
-        if (!c->dma) {
-            rc = br_zc_launch(ctx, ss[q], fr, c->slot, len_of(sl), ifx_of(sl), cc.n, act_of(sl), ver_of(sl),
-                              egr_of(sl), dstats);
+        if (!c->dma) {   // the kernel on the mapped ring (device addresses of the same pages)
+            uint8_t *dfr_zc = dring + sl * C * c->slot, *dm = dmeta + sl * C * 16;
+            rc = br_dev_launch(ctx, ss[q], dfr_zc, c->slot, (uint16_t *)dm, (uint32_t *)(dm + C * 4), cc.n, dm + C * 12,
+                               dm + C * 13, (int32_t *)(dm + C * 8), dstats);
         } else {   // frames and inputs in by DMA, the router in HBM, frames and outputs back by DMA
-            uint8_t *m = dmeta[q];
+            uint8_t *m = dmt[q];
             if (hipMemcpyAsync(dfr[q], fr, cc.n * c->slot, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
                 hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess)
                 rc = fail(-EIO, "loop: H2D copy");
@@ -308,11 +304,9 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     if (dstats) (void)hipFree(dstats);
     for (int i = 0; i < D; ++i) {
         if (dfr[i]) (void)hipFree(dfr[i]);
-        if (dmeta[i]) (void)hipFree(dmeta[i]);
+        if (dmt[i]) (void)hipFree(dmt[i]);
     }
-    hfv_host_unregister(ctx, meta);
-    hfv_host_unregister(ctx, ring);
-    free(ring);
-    free(meta);
+    (void)hipHostFree(ring);
+    (void)hipHostFree(meta);
     return rc;
 }

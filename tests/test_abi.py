@@ -113,3 +113,28 @@ def test_shard_ranges_cover_word_aligned():
             assert cuts[0][0] == 0 and cuts[-1][1] == n
             for (a0, a1), (b0, b1) in zip(cuts, cuts[1:]):
                 assert a1 == b0 and a0 % 64 == 0
+
+
+def test_new_entry_points_reject_bad_arguments_without_gpu():
+    """The round-2 entry points fail with -EINVAL on a NULL ctx or missing buffers before any
+    device work (CPU; the GPU behaviour is in test_gpu_loop / test_gpu_service / test_gpu_parity)."""
+    L = hfv.lib()
+    cfg = hfv.LoopConfig()
+    st = hfv.LoopStats()
+    assert L.hfv_loop_run(None, ctypes.byref(cfg), ctypes.byref(st)) == -errno.EINVAL
+    t = ctypes.c_uint64()
+    ms = ctypes.c_float()
+    assert L.hfv_service_run(None, None, 0, ctypes.byref(t), ctypes.byref(ms)) == -errno.EINVAL
+    assert L.hfv_verdict_counters(None, None, 64, 1, None, None, None) == -errno.EINVAL
+    assert "NULL" in L.hfv_last_error().decode() or "null" in L.hfv_last_error().decode()
+    assert ctypes.sizeof(hfv.LoopStats) == 8 * (5 + hfv.BR_COUNTERS) + 8 * 5
+
+
+def test_loop_frame_digest_is_order_free():
+    """hfv_loop_run's transmitted-frame digest (mirrored in scion_hfv.loop_frame_digest) depends
+    on the bytes and the egress port, and sums order-independently."""
+    a, b = bytes(range(138)), bytes(range(1, 139))
+    da, db = hfv.loop_frame_digest(a, 3), hfv.loop_frame_digest(b, 3)
+    assert da != db and hfv.loop_frame_digest(a, 1) != da
+    assert (da + db) % 2**64 == (db + da) % 2**64
+    assert hfv.loop_frame_digest(a[:137], 3) != da

@@ -25,6 +25,18 @@
 #include <hip/hip_ext.h>
 #include <stdlib.h>
 
+// Staging waves per CU: 12 (AES tables with 16 lane copies) or 16 (4 copies, to fit the
+// 16 header-row buffers in LDS; VGPRs then capped at 128).
+#ifndef HFV_BR_WAVES
+#define HFV_BR_WAVES 12
+#endif
+#ifndef HFV_TAB3_COPIES
+#if HFV_BR_WAVES == 16
+#define HFV_TAB3_COPIES 4
+#else
+#define HFV_TAB3_COPIES 16
+#endif
+#endif
 #include "hfv_aes_dev.h"
 #include "hfv_internal.h"
 
@@ -38,7 +50,7 @@ static __shared__ unsigned long long s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_C
 // writes and the per-lane reads bank-conflict free), for up to kBrStageWaves waves per block.
 constexpr int kBrWin = 128;
 constexpr int kBrRow = kBrWin / 4 + 1;
-constexpr int kBrStageWaves = 12;
+constexpr int kBrStageWaves = HFV_BR_WAVES;
 static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 
 // enum xdp_action and enum verdict (br/src/bpf/common.h:38-70)
@@ -757,8 +769,8 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     K k;
     int block;
     if (staged) {
-        block = 768;
-        k = stats ? k_br_process<768, true, kBrWin> : k_br_process<768, false, kBrWin>;
+        block = kBrStageWaves * 64;
+        k = stats ? k_br_process<kBrStageWaves * 64, true, kBrWin> : k_br_process<kBrStageWaves * 64, false, kBrWin>;
     } else {
         block = 1024;
         k = stats ? k_br_process<1024, true, 0> : k_br_process<1024, false, 0>;

@@ -664,13 +664,23 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
     lens = np.full(1000, E.FRAME_LEN, dtype=np.uint16)
     kw = dict(rx_ifindex=E.RX_IFINDEX, slot=slot, chunk=chunk, chunks=chunks, producers=producers,
               consumers=consumers, inflight=inflight, dma=dma)
-    ctx.loop_run(frames, lens, 4 * chunk, **kw)                          # warm the registration path
+    ctx.loop_run(frames, lens, 4 * chunk, **kw)                          # warm up
     W.barrier()
-    r = ctx.loop_run(frames, lens, total, **kw)
-    el = max(W.gather(r["seconds"]))
-    assert r["rx"] == total and r["tx"] == total and r["verdicts"][1] == total, r   # every frame forwarded
-    r["numa_node"] = ctx.numa_node()
+    # a failure on one rank must not leave the others waiting in the gather: every rank gets
+    # to it, with a negative time if its loop failed
+    try:
+        r = ctx.loop_run(frames, lens, total, **kw)
+        ok = r["rx"] == total and r["tx"] == total and r["verdicts"][1] == total   # every frame forwarded
+        err = None if ok else f"counts {r['rx']}/{r['tx']}/{r['verdicts']}"
+    except Exception as e:   # noqa: BLE001 -- reported in the line, not fatal to the headline
+        r, err = None, str(e)
+    times = W.gather(r["seconds"] if r and not err else -1.0)
+    ctx_numa = ctx.numa_node()
     ctx.close()
+    if min(times) < 0:
+        return {"error": err or "a rank's loop failed", "per_rank_s": times}
+    el = max(times)
+    r["numa_node"] = ctx_numa
     return {"mpkts": round(W.size * total / el / 1e6, 2), "seconds": round(el, 4), "frames_per_gpu": total,
             "chunk": chunk, "chunks": chunks, "producers": producers, "consumers": consumers, "slot": slot,
             "inflight": inflight, "router_io": "DMA through HBM" if dma else "zero-copy over PCIe",
@@ -694,8 +704,8 @@ def run_loop(args, W):
                      args.loop_slot, args.loop_inflight, args.loop_dma)
     result = {
         "metric": "Mpkt/s config-5 loop: RX ring -> border router on the GPU -> TX/drop, 138 B frames",
-        "value": r["mpkts"], "unit": "Mpkt/s", "n_gpus": W.size, "steps": 1, "warmup": 1,
-        "ms_per_step": round(r["seconds"] * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "value": r.get("mpkts"), "unit": "Mpkt/s", "n_gpus": W.size, "steps": 1, "warmup": 1,
+        "ms_per_step": round(r["seconds"] * 1e3, 3) if "seconds" in r else None, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (gen_packets.py's 1000 frames, cycled like tcpreplay --loop)",
         "config": {"workload": f"config 5: {args.loop_n} frames per GPU through hfv_loop_run as br1-ff00_0_1-2",
@@ -876,7 +886,7 @@ def run_hf(args, W):
                              "note": "hf_check_off = the reference's ENABLE_HF_CHECK=OFF build (br/CMakeLists.txt:8,"
                                      "48-64); hf_check_share = the part of the kernel time the MAC check costs"}
 
-    if extras and args.loop_n:
+    if args.loop_n and not args.no_extras:   # config 5 runs on every rank (8x batch-sharded at N = 8)
         W.sync()
         result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads,
                                               args.loop_consumers, args.loop_slot, args.loop_inflight, args.loop_dma)

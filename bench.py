@@ -230,6 +230,9 @@ def pmc_traffic(key):
         return None
 
 
+LOOKUPS_PER_PKT = 145   # T-table lookups per packet (11 + 8 x 16 + 6), each addressed by one v_perm
+
+
 def ceilings(keysel, n, mhz, cus):
     """Bounds beside HBM, per packet, read from the committed PMC summary of this
     configuration (SQ_INSTS_LDS / SQ_INSTS_VALU are wave-instructions: x 64 lanes / records
@@ -246,6 +249,10 @@ def ceilings(keysel, n, mhz, cus):
     if mhz:
         out["shader_mhz"] = round(mhz, 1)
         out["lds_issue_bound_mpkts"] = round(cus * 32 * mhz * 1e6 / lds / 1e6, 1)
+        # VALU issue: full-rate ops 128 lanes per clock per CU, v_perm (one per table lookup,
+        # 145 per packet) half rate (profiles/r01/ubench/valu_rate.log): CU-clocks per packet
+        # = (valu + perms) / 128
+        out["valu_issue_bound_mpkts"] = round(cus * mhz * 1e6 * 128 / (valu + LOOKUPS_PER_PKT) / 1e6, 1)
     out["hbm_peak_bound_mpkts"] = round(HBM_PEAK_GBS * 1e9 / BYTES_PER_PACKET / 1e6, 1)
     return out
 

@@ -230,6 +230,15 @@ def pmc_traffic(key):
         return None
 
 
+def settle(args):
+    """Idle the GPU before a leg (outside any timed region): the shader clock falls from ~2.0 to
+    ~1.5 GHz over a few ms of back-to-back full-chip work (power limit, scripts/svc_batch_size.py)
+    and recovers when idle, so each leg starts from the same state instead of inheriting the
+    previous leg's heat.  --settle-s 0 turns it off."""
+    if args.settle_s > 0:
+        time.sleep(args.settle_s)
+
+
 LOOKUPS_PER_PKT = 145   # T-table lookups per packet (11 + 8 x 16 + 6), each addressed by one v_perm
 
 
@@ -826,6 +835,7 @@ def run_hf(args, W):
         assert popcount(m["bitmaps"][0]) == expected_pass_count(n, first)
 
     if extras and args.big_n:
+        settle(args)
         nb = args.big_n
         big = torch.empty((nb, 64), dtype=torch.uint8, device="cuda")
         ctx.gen_records(big, nb, SEED_RECORDS, first_index=0, stream=stream)
@@ -857,6 +867,7 @@ def run_hf(args, W):
 
     ref_bits = bits0.cpu().numpy().view(np.uint64).copy()
     if extras and keysel == hfv.KEYSEL_ZERO:   # config 3 beside the config-2 headline
+        settle(args)
         ctx3 = make_ctx(hfv, W.device, hfv.KEYSEL_IFID)
         m3 = measure_hf(hfv, W, ctx3, "ifid", n, first, args.rotate, args.steps, args.warmup, stream,
                         reps=args.svc_reps)
@@ -876,6 +887,7 @@ def run_hf(args, W):
         result.update(host_leg(hfv, W, ctx, recs0, n, ref_bits))
 
     if extras and args.br_n:
+        settle(args)
         W.sync()
         r4, sample = measure_br(hfv, W, args.br_n, 5, 2)
         r4off, _ = measure_br(hfv, W, args.br_n, 5, 2, hf_check=False)
@@ -898,6 +910,8 @@ def run_hf(args, W):
         result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads,
                                               args.loop_consumers, args.loop_slot, args.loop_inflight, args.loop_dma)
 
+    if extras:
+        result["settle_s_before_extra_legs"] = args.settle_s
     if W.rank == 0 and W.size == 1 and args.cpu_budget > 0:
         result["cpu_baseline"] = cpu_baseline(recs0.cpu().numpy(), keysel, ref_bits, args.cpu_budget)
 
@@ -935,6 +949,7 @@ def main():
     ap.add_argument("--loop-dma", action="store_true", help="config-5 loop: chunks through HBM by DMA, not zero-copy")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
+    ap.add_argument("--settle-s", type=float, default=0.5, help="idle seconds before each extra leg (untimed)")
     ap.add_argument("--svc-reps", type=int, default=3, help="timed service regions of K steps (median reported)")
     ap.add_argument("--launch-only", action="store_true",
                     help="measure the launch path only (ranks sharing one GPU cannot each hold a service grid)")

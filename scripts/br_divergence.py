@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""How much of the config-4 kernel time is SIMT divergence: the bench's frame mix (48 PTF
+templates interleaved frame by frame, so every wave mixes IPv4/IPv6 and all path kinds) against
+the same frames sorted by template (each wave sees one or two templates) and a single template.
+python scripts/br_divergence.py   (1 GPU)"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "scion-xdp-br_amd"), ROOT]
+import torch  # noqa: E402
+import scion_hfv as hfv  # noqa: E402
+import bench  # noqa: E402
+from scion_hfv import topology as TP  # noqa: E402
+
+
+def main():
+    n = 1 << 20
+    ctx = hfv.Ctx(0)
+    ctx.key_add(0, TP.KEYS[1])
+    ctx.br_set_config(TP.br_config("br1"))
+    frames, ifis, good, abytes = bench.br_templates()
+    tmpl, tid, lens, ifidx, _ = bench.br_batch(n, 0)
+    order = {"interleaved (bench)": np.arange(n), "sorted by template": np.argsort(tid, kind="stable")}
+    d_tmpl = torch.from_numpy(tmpl).cuda()
+    ifis = np.array(ifis, dtype=np.int32)
+    shapes = []
+    for name, o in order.items():
+        shapes.append((name, tid[o], lens[o]))
+    t0 = int(tid[0])
+    shapes.append(("one template", np.full(n, t0), np.full(n, lens[0], dtype=np.uint16)))
+    v4 = [i for i in range(len(frames)) if frames[i][12:14] == b"\x08\x00"]
+    shapes.append(("IPv4 templates only, interleaved", np.array(v4)[np.arange(n) % len(v4)],
+                   np.maximum(np.array([len(frames[i]) for i in v4])[np.arange(n) % len(v4)], 64).astype(np.uint16)))
+    for name, t, ln in shapes:
+        dt = torch.from_numpy(t.astype(np.int64)).cuda()
+        master = d_tmpl[dt]
+        d_len = torch.from_numpy(ln.astype(np.uint16).view(np.int16)).cuda()
+        d_if = torch.from_numpy(ifis).cuda()[dt]
+        act = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        ver = torch.zeros_like(act)
+        egr = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ks = []
+        for r in range(8):
+            work = master.clone()
+            ms = ctx.br_process_timed(work, bench.BR_SLOT, d_len, d_if, n, act, ver, egr)
+            if r >= 2:
+                ks.append(ms)
+        print(f"{name:36s} kernel {np.median(ks) * 1e3:7.1f} us  ({n / np.median(ks) / 1e6:6.2f} Gpkt/s)", flush=True)
+        del master, work
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

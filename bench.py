@@ -328,7 +328,9 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     posts = ctx.service_batches([(batches[k % R], n, bitmaps[k % nb]) for k in range(steps)])
 
     def service_run():
+        t = time.perf_counter()
         svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
+        svc["call_us"] = (time.perf_counter() - t) * 1e6
 
     # the K-step timed region is repeated `reps` times (each a fresh grid over the same K
     # batches) and the median region is reported: one timed region of ~0.3 ms is exposed to a
@@ -339,12 +341,14 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
             b.zero_()
         W.sync()
         el, per_rank = W.timed(1, service_run)
-        runs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz()))   # clock: diagnostics, untimed
+        runs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"]))   # diagnostics
         check(steps)
     runs.sort(key=lambda r: r[0])
-    svc_el, per_rank, grid_ms, mhz = runs[len(runs) // 2]
+    svc_el, per_rank, grid_ms, mhz, _ = runs[len(runs) // 2]
     out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
-                "svc_all_ms": [round(r[0] * 1e3, 4) for r in sorted(runs, key=lambda r: r[0])]})
+                "svc_all_ms": [round(r[0] * 1e3, 4) for r in runs],
+                "svc_all_grid_ms": [round(r[2], 4) for r in runs],
+                "svc_all_call_us": [round(r[4], 1) for r in runs]})
     return out
 
 
@@ -809,7 +813,8 @@ def run_hf(args, W):
             "mpkts": round(total * args.steps / m["svc_el"] / 1e6, 2),
             "ms_per_step": round(m["svc_el"] / args.steps * 1e3, 5), "grid_ms": round(m["grid_ms"], 4),
             "shader_mhz": round(m["mhz"], 1) if m["mhz"] else None,
-            "timed_regions_ms": m.get("svc_all_ms"),
+            "timed_regions_ms": m.get("svc_all_ms"), "grids_ms": m.get("svc_all_grid_ms"),
+            "service_run_call_us": m.get("svc_all_call_us"),
             "note": f"value = the median of {args.svc_reps} timed regions of K steps each (each a fresh grid)"},
         "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),
                        "ms_per_step": round(m["launch_el"] / args.steps * 1e3, 5),

@@ -1676,11 +1676,23 @@ int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count,
                       batches[i].n, batches[i].stride, &t);
         if (i == 0) *first_ticket = t;
     }
+    struct timespec t_post, t_launch, t_done;
+    clock_gettime(CLOCK_MONOTONIC, &t_post);
     if (!launched) {
         int lr = svc_launch(ctx, ds);
         if (lr) return lr;
     }
+    clock_gettime(CLOCK_MONOTONIC, &t_launch);
     int sr = svc_stop(ctx, kernel_ms);
+    clock_gettime(CLOCK_MONOTONIC, &t_done);
+    static const bool trace = getenv("HFV_SVC_TRACE") != nullptr;   // diagnostics
+    if (trace) {
+        auto us = [](const timespec &a, const timespec &b) {
+            return (b.tv_sec - a.tv_sec) * 1e6 + (b.tv_nsec - a.tv_nsec) / 1e3;
+        };
+        fprintf(stderr, "hfv_service_run: launch call %.1f us, launch return -> grid exit seen %.1f us, grid %.1f us\n",
+                us(t_post, t_launch), us(t_launch, t_done), kernel_ms ? *kernel_ms * 1e3 : -1.0);
+    }
     return rc ? rc : sr;
 }
 

@@ -36,4 +36,15 @@ for rep in range(6):
     print("K %d rep %d: submitv+launch %.1f stop %.1f sync %.1f total %.1f us; grid %.1f us; wall-grid %.1f us"
           % (K, rep, (t1 - t0) * 1e6, (t2 - t1) * 1e6, (t3 - t2) * 1e6, (t3 - t0) * 1e6, g * 1e3,
              (t3 - t0) * 1e6 - g * 1e3), flush=True)
+# the one-shot form bench.py times (hfv_service_run: batches + stop posted, launch, wait)
+for rep in range(6):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, g = ctx.service_run(posts)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print("K %d rep %d: service_run %.1f sync %.1f total %.1f us; grid %.1f us; wall-grid %.1f us"
+          % (K, rep, (t1 - t0) * 1e6, (t2 - t1) * 1e6, (t2 - t0) * 1e6, g * 1e3, (t2 - t0) * 1e6 - g * 1e3),
+          flush=True)
 ctx.close()

@@ -149,7 +149,7 @@ struct hfv_ctx {
     hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
     DevState *dev_tab[2] = {nullptr, nullptr};
     hipStream_t readers[2][8] = {};                // streams that launched with dev_tab[i]
-    hipEvent_t reader_ev[2][8] = {};               // recorded on readers[i][r] after each such launch
+    hipEvent_t reader_ev[2][8] = {};               // caller streams: recorded after each such launch
     int nreaders[2] = {0, 0};
     bool readers_overflow[2] = {false, false};
     int active = 0;
@@ -226,6 +226,7 @@ static hipStream_t pick_stream(hfv_ctx *, void *stream) { return (hipStream_t)st
 // table is rewritten, the publishing stream waits for an event recorded on each of them, so
 // no per-launch event is needed on the hot path.
 static void note_reader(hfv_ctx *ctx, hipStream_t st);
+static bool own_stream(const hfv_ctx *ctx, hipStream_t st);
 
 // Make the shadow table visible to work enqueued next on `st`; returns the table to use.
 static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
@@ -267,7 +268,11 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
             // the events were recorded after each reader's last launch with the table, so the
             // fence holds even for a reader stream the caller has destroyed since
             for (int r = 0; r < ctx->nreaders[next]; ++r) {
-                if (ctx->readers[next][r] == st) continue;   // same stream: ordered already
+                hipStream_t rs = ctx->readers[next][r];
+                if (rs == st) continue;   // same stream: ordered already
+                // the ctx's own streams live as long as the ctx: mark them now; a caller's
+                // stream carries the event recorded after its last launch with the table
+                if (own_stream(ctx, rs)) HIP_TRY(hipEventRecord(ctx->reader_ev[next][r], rs));
                 HIP_TRY(hipStreamWaitEvent(st, ctx->reader_ev[next][r], 0));
             }
         }
@@ -282,6 +287,11 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
     return 0;
 }
 
+static bool own_stream(const hfv_ctx *ctx, hipStream_t st)
+{
+    return st && (st == ctx->stream || st == ctx->svc_stream || st == ctx->hstream[0] || st == ctx->hstream[1]);
+}
+
 static void note_reader(hfv_ctx *ctx, hipStream_t st)
 {
     const int a = ctx->active;
@@ -294,7 +304,9 @@ static void note_reader(hfv_ctx *ctx, hipStream_t st)
         }
         ctx->readers[a][ctx->nreaders[a]++] = st;
     }
-    if (hipEventRecord(ctx->reader_ev[a][r], st) != hipSuccess) ctx->readers_overflow[a] = true;
+    // a caller's stream may be destroyed before the next publish: remember where its launches
+    // with this table end (one event record per launch; the ctx's own streams skip it)
+    if (!own_stream(ctx, st) && hipEventRecord(ctx->reader_ev[a][r], st) != hipSuccess) ctx->readers_overflow[a] = true;
 }
 
 static int after_launch(hfv_ctx *ctx, hipStream_t st, int err, const char *what)

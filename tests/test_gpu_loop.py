@@ -88,3 +88,52 @@ def test_loop_rejects_bad_geometry(gpu_ctx):
         args.update(kw)
         with pytest.raises(hfv.HfvError):
             gpu_ctx.loop_run(frames, np.full(2, E.FRAME_LEN), 10, **args)
+
+
+@pytest.mark.parametrize("dma", [False, True], ids=["zero_copy", "dma"])
+def test_loop_ptf_mix_ipv4_ipv6(gpu_ctx, dma):
+    """The loop over the config-4 frame mix (the reference test topology's BR 1: IPv4 and IPv6
+    underlays, AS ingress, sibling hand-over, segment switch, corrupted MACs), frames of mixed
+    length in 256-byte slots, several ingress interfaces: counts and transmitted-frame digests
+    equal the oracle router's."""
+    import br_topo as T
+    sys_path_bench()
+    import bench
+    frames, ifis, good, _ = bench.br_templates()
+    n = len(frames)
+    stride = 256
+    buf = np.zeros((n, stride), dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint16)
+    for i, f in enumerate(frames):
+        buf[i, :len(f)] = np.frombuffer(f, dtype=np.uint8)
+        lens[i] = len(f)
+    assert lens.max() <= stride
+    # the loop takes one ingress ifindex per run: run it once per ingress interface of the mix
+    cfg = T.br_config("br1")
+    for ifx in sorted(set(ifis)):
+        sel = np.array([i for i in range(n) if ifis[i] == ifx])
+        gpu_ctx.br_set_config(cfg)
+        gpu_ctx.key_add(0, T.KEYS[1])
+        gpu_ctx.br_set_hf_check(True)
+        total = 5 * len(sel) + 3
+        got = gpu_ctx.loop_run(buf[sel], lens[sel], total, rx_ifindex=int(ifx), slot=stride, chunk=7, chunks=3,
+                               producers=2, consumers=2, digest=True, dma=dma)
+        slots = buf[sel].copy()
+        a, v, e, _ = orc.br_process(slots, lens[sel], np.full(len(sel), ifx, dtype=np.uint32), cfg,
+                                    orc.hop_key(T.KEYS[1]))
+        reps = np.bincount(np.arange(total) % len(sel), minlength=len(sel)).astype(np.uint64)
+        tx = a == 4
+        digest = 0
+        for i in np.nonzero(tx)[0]:
+            digest = (digest + int(reps[i]) * hfv.loop_frame_digest(bytes(slots[i, :lens[sel][i]]), int(e[i]))) % 2**64
+        assert got["rx"] == total and got["tx"] == int(reps[tx].sum()), ifx
+        assert got["tx_digest"] == digest, ifx
+        assert got["drop"] == int(reps[~tx].sum())
+
+
+def sys_path_bench():
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)

@@ -128,6 +128,32 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
     }
     for (uint32_t i = 0; i < in->n_tx_ports; ++i)
         if (in->tx_ports[i] < HFV_BR_MAX_TXPORTS) out->tx_bits[in->tx_ports[i] >> 5] |= 1u << (in->tx_ports[i] & 31);
+    // egress entries: the route to the link's remote (fib_lookup_as_egress / fib_lookup_egress_br
+    // look up the entry's own remote address, fib_lookup.h:29-180) and the sibling's internal
+    // interface, with the kernel's longest-prefix rule (ties keep the first route)
+    for (uint32_t i = 0; i < out->n_egr; ++i) {
+        DevBrEgress &e = out->egress[i];
+        int best = -1;
+        uint32_t best_len = 0;
+        for (uint32_t r = 0; r < out->n_routes; ++r) {
+            const DevBrRoute &rt = out->routes[r];
+            if (rt.family != e.family) continue;
+            uint32_t diff = 0;
+            for (int w = 0; w < 4; ++w) diff |= (e.remote_be[w] ^ rt.pfx[w]) & rt.mask[w];
+            if (diff == 0 && (best < 0 || rt.plen > best_len)) {
+                best = (int)r;
+                best_len = rt.plen;
+            }
+        }
+        e.route = best;
+        const uint32_t out_if = best >= 0 ? out->routes[best].ifindex : 0;
+        e.sib_iface = -1;
+        for (uint32_t k = 0; k < out->n_int; ++k)
+            if (out->int_ifaces[k].ifindex == out_if) {
+                e.sib_iface = (int)k;
+                break;
+            }
+    }
 }
 
 }  // namespace hfv

@@ -454,7 +454,7 @@ __device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link
     k.udp_src = link.local_port;
     set_dst(k, link.remote);
     set_src(k, link.local);
-    int r = route_lookup(k.family, link.remote_be[0], link.remote_be[1], link.remote_be[2], link.remote_be[3]);
+    const int r = link.route;   // route_lookup of link.remote_be, resolved with the tables
     if (!fib_result(k, r)) return -1;
     return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
 }
@@ -463,10 +463,10 @@ __device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
 {
     k.udp_dst = sib.remote_port;
     set_dst(k, sib.remote);
-    int r = route_lookup(k.family, sib.remote_be[0], sib.remote_be[1], sib.remote_be[2], sib.remote_be[3]);
+    const int r = sib.route;   // route_lookup of sib.remote_be, resolved with the tables
     if (!fib_result(k, r)) return -1;
     uint32_t out_if = r >= 0 ? s_br.routes[r].ifindex : 0;
-    int s = int_iface(out_if);
+    const int s = sib.sib_iface;   // int_iface(out_if)
     if (s < 0) {
         k.verdict = V_ABORT;
         return -1;

@@ -45,6 +45,10 @@ struct DevBrEgress {
     uint32_t remote[4], local[4];   // l32 words
     uint32_t remote_be[4];          // big-endian words of remote (route lookup key)
     uint32_t remote_port, local_port;   // l16
+    // resolved at compile time from the static tables (the per-frame lookups' results depend
+    // only on the entry): the next-hop route of `remote` (-1: none) and, for a sibling, the
+    // internal interface on that route's ifindex (-1: none)
+    int32_t route, sib_iface;
 };
 struct DevBrRoute {
     uint32_t family;    // 0: never matches (prefix length beyond the family's width)

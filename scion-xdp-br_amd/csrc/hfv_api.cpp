@@ -128,6 +128,12 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
     }
     for (uint32_t i = 0; i < in->n_tx_ports; ++i)
         if (in->tx_ports[i] < HFV_BR_MAX_TXPORTS) out->tx_bits[in->tx_ports[i] >> 5] |= 1u << (in->tx_ports[i] & 31);
+    memset(out->int_of_ifindex, 0xff, sizeof out->int_of_ifindex);
+    memset(out->egr_of_ifid, 0xff, sizeof out->egr_of_ifid);
+    for (uint32_t i = out->n_int; i-- > 0;)   // reverse: the first match wins
+        if (out->int_ifaces[i].ifindex < 64) out->int_of_ifindex[out->int_ifaces[i].ifindex] = (int8_t)i;
+    for (uint32_t i = out->n_egr; i-- > 0;)
+        if (out->egress[i].ifid < 256) out->egr_of_ifid[out->egress[i].ifid] = (int8_t)i;
     // egress entries: the route to the link's remote (fib_lookup_as_egress / fib_lookup_egress_br
     // look up the entry's own remote address, fib_lookup.h:29-180) and the sibling's internal
     // interface, with the kernel's longest-prefix rule (ties keep the first route)

@@ -365,6 +365,7 @@ __device__ __forceinline__ bool as_egress(BrFrame &k, uint32_t as_ing_ifid)
 // ---- tables (LDS) ----------------------------------------------------------------------------
 __device__ __forceinline__ int int_iface(uint32_t ifindex)
 {
+    if (ifindex < 64) return s_br.int_of_ifindex[ifindex];
     for (uint32_t i = 0; i < s_br.n_int; ++i)
         if (s_br.int_ifaces[i].ifindex == ifindex) return (int)i;
     return -1;
@@ -383,6 +384,7 @@ __device__ __forceinline__ int ingress_lookup(const BrFrame &k)
 
 __device__ __forceinline__ int egress_lookup(uint32_t ifid)
 {
+    if (ifid < 256) return s_br.egr_of_ifid[ifid];
     for (uint32_t i = 0; i < s_br.n_egr; ++i)
         if (s_br.egress[i].ifid == ifid) return (int)i;
     return -1;

@@ -66,6 +66,10 @@ struct DevBrConfig {
     DevBrIngress ingress[HFV_BR_MAX_IFACES];
     DevBrEgress egress[HFV_BR_MAX_IFACES];
     DevBrRoute routes[HFV_BR_MAX_ROUTES];
+    // direct maps for the common small keys (first match, -1: none): int_iface_map for ingress
+    // ifindex < 64, egress_map for IFID < 256; larger keys use the linear searches
+    int8_t int_of_ifindex[64];
+    int8_t egr_of_ifid[256];
 };
 static_assert(sizeof(DevBrConfig) % 16 == 0, "copied to LDS in 16 B pieces");
 

@@ -134,6 +134,11 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
         if (out->int_ifaces[i].ifindex < 64) out->int_of_ifindex[out->int_ifaces[i].ifindex] = (int8_t)i;
     for (uint32_t i = out->n_egr; i-- > 0;)
         if (out->egress[i].ifid < 256) out->egr_of_ifid[out->egress[i].ifid] = (int8_t)i;
+    memset(out->ing_of_ifindex, 0xff, sizeof out->ing_of_ifindex);
+    for (uint32_t i = 0; i < out->n_ing; ++i) {
+        const uint32_t x = out->ingress[i].ifindex16;
+        if (x < 64) out->ing_of_ifindex[x] = out->ing_of_ifindex[x] == -1 ? (int8_t)i : (int8_t)-2;
+    }
     // egress entries: the route to the link's remote (fib_lookup_as_egress / fib_lookup_egress_br
     // look up the entry's own remote address, fib_lookup.h:29-180) and the sibling's internal
     // interface, with the kernel's longest-prefix rule (ties keep the first route)

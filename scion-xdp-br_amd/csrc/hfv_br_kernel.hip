@@ -371,8 +371,20 @@ __device__ __forceinline__ int int_iface(uint32_t ifindex)
     return -1;
 }
 
+__device__ __forceinline__ bool ingress_match(const DevBrIngress &e, const BrFrame &k)
+{
+    return e.v4 == k.v4_dst && e.v6[0] == k.v6_dst[0] && e.v6[1] == k.v6_dst[1] && e.v6[2] == k.v6_dst[2] &&
+           e.v6[3] == k.v6_dst[3] && e.port == k.udp_dst && e.ifindex16 == (k.ifindex & 0xffffu);
+}
+
 __device__ __forceinline__ int ingress_lookup(const BrFrame &k)
 {
+    const uint32_t x = k.ifindex & 0xffffu;
+    if (x < 64) {   // the only entry on this interface, if there is just one
+        const int c = s_br.ing_of_ifindex[x];
+        if (c == -1) return -1;
+        if (c >= 0) return ingress_match(s_br.ingress[c], k) ? c : -1;
+    }
     for (uint32_t i = 0; i < s_br.n_ing; ++i) {
         const DevBrIngress &e = s_br.ingress[i];
         if (e.v4 == k.v4_dst && e.v6[0] == k.v6_dst[0] && e.v6[1] == k.v6_dst[1] && e.v6[2] == k.v6_dst[2] &&

@@ -70,6 +70,8 @@ struct DevBrConfig {
     // ifindex < 64, egress_map for IFID < 256; larger keys use the linear searches
     int8_t int_of_ifindex[64];
     int8_t egr_of_ifid[256];
+    // ingress_map candidates by ifindex < 64: the one entry on that ifindex (-1: none, -2: several)
+    int8_t ing_of_ifindex[64];
 };
 static_assert(sizeof(DevBrConfig) % 16 == 0, "copied to LDS in 16 B pieces");
 

@@ -99,8 +99,8 @@ struct BrFrame {
     int egress_ifindex;
     // deferred MAC check: ingress (mask bit 0) and egress-from-internal (bit 1) never both apply
     bool need_mac;
-    uint32_t mi[4];
-    uint32_t mac_lo, mac_hi;
+    int mac_inf, mac_hf;
+    uint32_t mac_beta;
 };
 
 // Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
@@ -294,15 +294,15 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
 // ---- path_processing.h ---------------------------------------------------------------------
 __device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return rd8(k, inf) & 1u; }
 
+// Only the fields' positions are kept: the macinput is read when the MAC is checked, after the
+// rewrite, which never touches the timestamp or the hop field (one copy of the reads for the
+// ingress and egress paths of a wave instead of one per path).
 __device__ __forceinline__ void defer_verify(BrFrame &k, int inf, int hf, uint32_t beta_nbo)
 {
     k.need_mac = true;
-    k.mi[0] = (beta_nbo & 0xffffu) << 16;
-    k.mi[1] = rd32(k, inf + 4);
-    k.mi[2] = (rd8(k, hf + 1) << 8) | (rd16(k, hf + 2) << 16);
-    k.mi[3] = rd16(k, hf + 4);
-    k.mac_lo = rd32(k, hf + 6);
-    k.mac_hi = rd16(k, hf + 10);
+    k.mac_inf = inf;
+    k.mac_hf = hf;
+    k.mac_beta = beta_nbo;
 }
 
 __device__ __forceinline__ bool as_ingress(BrFrame &k)
@@ -462,49 +462,11 @@ __device__ __forceinline__ void set_src(BrFrame &k, const uint32_t a[4])
     k.v6_hop = v4 ? k.v6_hop : 64u;
 }
 
-__device__ __forceinline__ int fib_as_egress(BrFrame &k, const DevBrEgress &link)
+// fib_lookup_ip's route: hdr->ip.v4->daddr or the IPv6 destination
+__device__ __forceinline__ int ip_route(const BrFrame &k)
 {
-    k.udp_dst = link.remote_port;
-    k.udp_src = link.local_port;
-    set_dst(k, link.remote);
-    set_src(k, link.local);
-    const int r = link.route;   // route_lookup of link.remote_be, resolved with the tables
-    if (!fib_result(k, r)) return -1;
-    return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
-}
-
-__device__ __forceinline__ int fib_egress_br(BrFrame &k, const DevBrEgress &sib)
-{
-    k.udp_dst = sib.remote_port;
-    set_dst(k, sib.remote);
-    const int r = sib.route;   // route_lookup of sib.remote_be, resolved with the tables
-    if (!fib_result(k, r)) return -1;
-    uint32_t out_if = r >= 0 ? s_br.routes[r].ifindex : 0;
-    const int s = sib.sib_iface;   // int_iface(out_if)
-    if (s < 0) {
-        k.verdict = V_ABORT;
-        return -1;
-    }
-    const DevBrIntIface &src = s_br.int_ifaces[s];
-    if (src.family != k.family) {
-        k.verdict = V_UNDERLAY_MISMATCH;
-        return -1;
-    }
-    k.udp_src = src.port;
-    set_src(k, src.addr);
-    return (int)out_if;
-}
-
-__device__ __forceinline__ int fib_ip_forward(BrFrame &k)
-{
-    int r;
-    if (k.family == HFV_AF_INET)   // hdr->ip.v4->daddr
-        r = route_lookup(k.family, sw32(rd32(k, k.ip + 16)), 0, 0, 0);
-    else
-        r = route_lookup(k.family, sw32(k.v6_dst[0]), sw32(k.v6_dst[1]), sw32(k.v6_dst[2]), sw32(k.v6_dst[3]));
-    if (!fib_result(k, r)) return -1;
-    k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
-    return r >= 0 ? (int)s_br.routes[r].ifindex : 0;
+    if (k.family == HFV_AF_INET) return route_lookup(k.family, sw32(rd32(k, k.ip + 16)), 0, 0, 0);
+    return route_lookup(k.family, sw32(k.v6_dst[0]), sw32(k.v6_dst[1]), sw32(k.v6_dst[2]), sw32(k.v6_dst[3]));
 }
 
 // ---- rewrite.h -------------------------------------------------------------------------------
@@ -599,18 +561,38 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
     if (f < 0) return (int)record<STATS>(k, V_ABORT);
     const DevBrEgress &fwd = s_br.egress[f];
 
-    int egress;
-    if (fwd.fwd_external) {
-        if (!as_egress(k, as_ing_ifid)) return (int)record<STATS>(k, k.verdict);
+    // The three next-hop cases (fib_lookup_as_egress / fib_lookup_egress_br / fib_lookup_ip,
+    // fib.h) share one route-result step and one address update, so a wave holding frames of
+    // several cases runs those once.
+    const bool ext = fwd.fwd_external, sib = !ext && as_ing_ifid != 0;
+    if (ext && !as_egress(k, as_ing_ifid)) return (int)record<STATS>(k, k.verdict);
+    int r;
+    if (ext || sib) {
         if (fwd.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
-        egress = fib_as_egress(k, fwd);
-    } else if (as_ing_ifid != 0) {
-        if (fwd.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
-        egress = fib_egress_br(k, fwd);
+        k.udp_dst = fwd.remote_port;
+        set_dst(k, fwd.remote);
+        r = fwd.route;   // route_lookup of the link's remote address, resolved with the tables
     } else {
-        egress = fib_ip_forward(k);
+        r = ip_route(k);
     }
-    if (egress < 0) return (int)record<STATS>(k, k.verdict);
+    if (!fib_result(k, r)) return (int)record<STATS>(k, k.verdict);
+    const int egress = r >= 0 ? (int)s_br.routes[r].ifindex : 0;
+    if (ext || sib) {
+        const uint32_t *src_addr = fwd.local;
+        uint32_t src_port = fwd.local_port;
+        if (sib) {   // the sibling's packets leave from the internal interface on the route
+            const int s = fwd.sib_iface;   // int_iface(egress)
+            if (s < 0) return (int)record<STATS>(k, V_ABORT);
+            const DevBrIntIface &src = s_br.int_ifaces[s];
+            if (src.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
+            src_addr = src.addr;
+            src_port = src.port;
+        }
+        k.udp_src = src_port;
+        set_src(k, src_addr);
+    } else {
+        k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
+    }
     rewrite(k);
     k.egress_ifindex = egress;
     return -1;
@@ -641,10 +623,17 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
         bool ok = true;
         if (k.need_mac && !s_br.hf_check_off) {
             // slot-0 key (xdp.c:82) through the scalar cache, only where a hop field is checked
+            const int inf = k.mac_inf, hf = k.mac_hf;
+            uint32_t mi[4];
+            mi[0] = (k.mac_beta & 0xffffu) << 16;
+            mi[1] = rd32(k, inf + 4);
+            mi[2] = (rd8(k, hf + 1) << 8) | (rd16(k, hf + 2) << 16);
+            mi[3] = rd16(k, hf + 4);
+            const uint32_t mac_lo = rd32(k, hf + 6), mac_hi = rd16(k, hf + 10);
             const UniformKey ukey(keys);
             uint32_t t0, t1;
-            cmac48_macinput<3>(k.mi, ukey, l, t0, t1);
-            ok = ukey.ok && t0 == k.mac_lo && (t1 & 0xffffu) == k.mac_hi;
+            cmac48_macinput<3>(mi, ukey, l, t0, t1);
+            ok = ukey.ok && t0 == mac_lo && (t1 & 0xffffu) == mac_hi;
         }
         if (!ok) v = V_INVALID_HF;
         else if (tx_port(k.egress_ifindex)) v = V_FORWARD;

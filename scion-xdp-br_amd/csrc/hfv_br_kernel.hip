@@ -101,6 +101,8 @@ struct BrFrame {
     bool need_mac;
     int mac_inf, mac_hf;
     uint32_t mac_beta;
+    uint32_t clob;      // bit 0 / 1: the rewrite's SegID store at INF+2 / INF+10 lands in the hop field
+    uint32_t orig_ab;   // those bytes before the rewrite (INF+2..3 | INF+10..11 << 16)
 };
 
 // Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
@@ -295,8 +297,9 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
 __device__ __forceinline__ uint32_t cons_at(const BrFrame &k, int inf) { return rd8(k, inf) & 1u; }
 
 // Only the fields' positions are kept: the macinput is read when the MAC is checked, after the
-// rewrite, which never touches the timestamp or the hop field (one copy of the reads for the
-// ingress and egress paths of a wave instead of one per path).
+// rewrite (one copy of the reads for the ingress and egress paths of a wave instead of one per
+// path).  The rewrite never stores into the timestamp; it stores into the hop field only when
+// CurrINF points past the info fields, and keep_mac_bytes saves those bytes first.
 __device__ __forceinline__ void defer_verify(BrFrame &k, int inf, int hf, uint32_t beta_nbo)
 {
     k.need_mac = true;
@@ -528,6 +531,28 @@ __device__ __forceinline__ void rewrite(BrFrame &k)
     wr16(k, k.udp + 6, fold_checksum(cs));
 }
 
+// The rewrite's only stores into the SCION path after PathMeta are the SegIDs at INF+2 and, on a
+// segment switch, INF+10.  With CurrINF past the info fields (parse_scion_path does not bound
+// it) either can fall inside the hop field whose MAC is checked; the BPF code read that
+// macinput before the rewrite (path_processing.h:39-57), so the bytes it would have seen are
+// kept here and substituted at the check (mac_b8).
+__device__ __forceinline__ void keep_mac_bytes(BrFrame &k)
+{
+    const int a = k.inf + 2, b = k.inf + 10, lo = k.mac_hf + 1, hi = k.mac_hf + 11;   // hop-field bytes read
+    const bool wb = k.segment_switch && k.inf + 16 <= k.len;
+    k.clob = (a + 1 >= lo && a <= hi ? 1u : 0u) | (wb && b + 1 >= lo && b <= hi ? 2u : 0u);
+    if (k.clob) k.orig_ab = rd16(k, a) | ((k.clob & 2u) ? rd16(k, b) << 16 : 0u);
+}
+
+__device__ __forceinline__ uint32_t mac_b8(const BrFrame &k, int off)
+{
+    if ((k.clob & 1u) && (off == k.inf + 2 || off == k.inf + 3)) return (k.orig_ab >> (8 * (off - k.inf - 2))) & 0xffu;
+    if ((k.clob & 2u) && (off == k.inf + 10 || off == k.inf + 11))
+        return (k.orig_ab >> (16 + 8 * (off - k.inf - 10))) & 0xffu;
+    return rd8(k, off);
+}
+__device__ __forceinline__ uint32_t mac_b16(const BrFrame &k, int off) { return mac_b8(k, off) | (mac_b8(k, off + 1) << 8); }
+
 // ---- xdp.c: process_packet -----------------------------------------------------------------
 // Returns the action (> 0 ends the frame), 0 (fall through to the MAC check without a record:
 // the bare `return 0`/ABORT paths) or -1 (rewritten, go to the MAC check).
@@ -593,6 +618,7 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
     } else {
         k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
     }
+    if (k.need_mac) keep_mac_bytes(k);
     rewrite(k);
     k.egress_ifindex = egress;
     return -1;
@@ -624,12 +650,20 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
         if (k.need_mac && !s_br.hf_check_off) {
             // slot-0 key (xdp.c:82) through the scalar cache, only where a hop field is checked
             const int inf = k.mac_inf, hf = k.mac_hf;
-            uint32_t mi[4];
+            uint32_t mi[4], mac_lo, mac_hi;
             mi[0] = (k.mac_beta & 0xffffu) << 16;
             mi[1] = rd32(k, inf + 4);
-            mi[2] = (rd8(k, hf + 1) << 8) | (rd16(k, hf + 2) << 16);
-            mi[3] = rd16(k, hf + 4);
-            const uint32_t mac_lo = rd32(k, hf + 6), mac_hi = rd16(k, hf + 10);
+            if (!k.clob) {
+                mi[2] = (rd8(k, hf + 1) << 8) | (rd16(k, hf + 2) << 16);
+                mi[3] = rd16(k, hf + 4);
+                mac_lo = rd32(k, hf + 6);
+                mac_hi = rd16(k, hf + 10);
+            } else {   // the hop field overlaps the rewritten SegIDs: the bytes from before the rewrite
+                mi[2] = (mac_b8(k, hf + 1) << 8) | (mac_b16(k, hf + 2) << 16);
+                mi[3] = mac_b16(k, hf + 4);
+                mac_lo = mac_b16(k, hf + 6) | (mac_b16(k, hf + 8) << 16);
+                mac_hi = mac_b16(k, hf + 10);
+            }
             const UniformKey ukey(keys);
             uint32_t t0, t1;
             cmac48_macinput<3>(mi, ukey, l, t0, t1);

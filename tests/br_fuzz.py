@@ -72,6 +72,30 @@ def long_path_frames(v6, mac_fn, count=8):
     return out
 
 
+# A transit frame whose CurrINF (2) points past its one info field, so the "info field" the
+# router uses lies inside the hop fields: its SegID is bytes 4-5 of the current hop field's MAC
+# and its timestamp the first 4 bytes of the next hop field.  The MAC was searched (tests only,
+# 2.5 s with orc.cmac: next hop's ConsIngress 5, beta 0x128d) so that it verifies against the
+# bytes as they arrive, with Cons set through MAC byte 2; scion_as_egress then rewrites that
+# SegID (beta ^ MAC[0:2]), i.e. into the hop field under check.  The BPF code read the macinput
+# before the rewrite (path_processing.h:39-57), so the frame is forwarded.
+OVERLAP_MAC = bytes.fromhex("a2632378128d")
+
+
+def overlap_frame(v6):
+    """(frame, first BR, ingress ifindex, expected frame) for the hop-field / SegID overlap."""
+    from scion_hfv import topology as TP
+    ing_enc, egr_enc, first, ifi = TP.encaps(1, 2, v6)
+    hops = [P.HopField(1, 2, exp=63, mac=OVERLAP_MAC), P.HopField(5, 7, exp=63), P.HopField(3, 4)]
+    path = P.Path([P.InfoField(True, seg_id=0x4242, ts=0x61000000)], hops, [3], curr_inf=2, curr_hf=0)
+    frame = ing_enc.frame(P.scion_header(path.pack()))
+    nb = 0x128d ^ struct.unpack(">H", OVERLAP_MAC[:2])[0]
+    hops_out = [P.HopField(1, 2, exp=63, mac=OVERLAP_MAC[:4] + struct.pack(">H", nb)), hops[1], hops[2]]
+    out = P.Path([P.InfoField(True, seg_id=0x4242, ts=0x61000000)], hops_out, [3], curr_inf=2, curr_hf=1)
+    want = egr_enc.frame(P.scion_header(out.pack()))
+    return frame, first, ifi, want
+
+
 IFINDICES = [1, 3, 4, 5, 6, 7, 9, 11, 13, 15, 2, 63, 64, 200]
 
 

@@ -194,3 +194,15 @@ def test_fuzz_is_deterministic_and_covers_verdicts(topo):
     want = {V[k] for k in ("SCION_FORWARD", "PARSE_ERROR", "NOT_SCION", "NOT_IMPLEMENTED", "NO_INTERFACE",
                            "ROUTER_ALERT", "INVALID_HF", "ABORT")}
     assert want <= seen, sorted(want - seen)
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+def test_segid_rewrite_inside_checked_hop_field(v6):
+    """CurrINF past the info fields: the SegID scion_as_egress rewrites is part of the hop field
+    whose MAC is checked afterwards; the check uses the bytes read before the rewrite."""
+    frame, first, ifi, want = F.overlap_frame(v6)
+    br = T.OracleBR(T.br_config(first, v6))
+    buf, lens = T.to_slots([frame])
+    a, v, e, _ = br.process(buf, lens, np.array([ifi], dtype=np.uint32))
+    assert (a[0], v[0]) == (4, V["SCION_FORWARD"])
+    assert buf[0, :len(want)].tobytes() == want

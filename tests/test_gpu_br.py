@@ -44,6 +44,25 @@ def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0, hf_check=True):
 
 
 @pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
+def test_segid_rewrite_inside_checked_hop_field(gpu_ctx, v6):
+    """The kernel reads the macinput at the MAC check, after the rewrite: a frame whose rewritten
+    SegID lies in the checked hop field (br_fuzz.overlap_frame) must still verify against the
+    bytes from before the rewrite, like the oracle; in a 64-frame tile with ordinary frames."""
+    frame, first, ifi, want = F.overlap_frame(v6)
+    cfg = T.br_config(first, v6)
+    brs = {b: T.OracleBR(T.br_config(b, v6)) for b in ("br1", "br2", "br3")}
+    hops = F.hop_inputs(brs, v6, MAC)
+    rest = [(f, i) for b, i, f in hops if b == first][:63]
+    frames, lens = T.to_slots([frame] + [f for f, _ in rest])
+    ifidx = np.array([ifi] + [i for _, i in rest], dtype=np.uint32)
+    v = _compare(gpu_ctx, frames, lens, ifidx, cfg, T.KEYS[1])
+    assert v[0] == hfv.VERDICT["SCION_FORWARD"] and frames[0, :len(want)].tobytes() != want   # input untouched
+    got = frames.copy()
+    T.GpuBR(gpu_ctx, cfg).process(got, lens, ifidx)
+    assert got[0, :len(want)].tobytes() == want
+
+
+@pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
 @pytest.mark.parametrize("br", ["br1", "br2", "br3"])
 def test_fuzz_parity(gpu_ctx, br, v6):
     brs = {b: T.OracleBR(T.br_config(b, v6)) for b in ("br1", "br2", "br3")}

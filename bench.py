@@ -673,10 +673,11 @@ def host_leg(hfv, W, ctx, recs, n, ref_bits):
                                            "whole 64 B lines), bitmap written to registered host memory"}}
 
 
-def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, inflight=3, dma=False):
+def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, inflight=2, dma=2):
     """Config 5 in one process (hfv_loop_run): gen_packets.py's 1000 frames cycled by producer
-    threads into a registered RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each
-    chunk zero-copy, consumer threads counting transmitted frames and dropping the rest."""
+    threads into a pinned RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each chunk
+    (dma: 0 zero-copy, 1 through HBM both ways, 2 copied in and the changes written back by the
+    kernel), consumer threads counting transmitted frames and dropping the rest."""
     from scion_hfv import evaluation as E
     ctx = hfv.Ctx(W.device)
     E.setup_ctx(ctx)
@@ -703,16 +704,16 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
     r["numa_node"] = ctx_numa
     return {"mpkts": round(W.size * total / el / 1e6, 2), "seconds": round(el, 4), "frames_per_gpu": total,
             "chunk": chunk, "chunks": chunks, "producers": producers, "consumers": consumers, "slot": slot,
-            "inflight": inflight, "router_io": "DMA through HBM" if dma else "zero-copy over PCIe",
+            "inflight": inflight, "router_io": ("zero-copy over PCIe", "DMA through HBM both ways",
+                          "DMA in, changed bytes written back by the kernel")[int(dma)],
             "tx_gbit_s": round(W.size * total * E.FRAME_LEN * 8 / el / 1e9, 1), "numa_node": r.get("numa_node"),
             "stage_busy_frac": {"router": round(r["gpu_busy_s"] / r["seconds"], 3),
                                 "router_waiting_for_rx": round(r["gpu_wait_s"] / r["seconds"], 3),
                                 "producer": round(r["producer_busy_s"] / producers / r["seconds"], 3),
                                 "consumer": round(r["consumer_busy_s"] / consumers / r["seconds"], 3)},
             "path": f"producer threads memcpy 138 B frames into a pinned, mapped host RX ring ({slot} B slots) -> "
-                    "the router kernel per chunk (zero-copy: reads headers over PCIe, writes rewritten rows back; or "
-                    "DMA through HBM) -> consumer threads count TX / drop; producers and consumers on the GPU's NUMA "
-                    "node",
+                    "the router kernel per chunk (router_io) -> consumer threads count TX / drop; producers and "
+                    "consumers on the GPU's NUMA node",
             "veth": "not used: the GPU box runs commands as an unprivileged user with user namespaces disabled "
                     "(unshare -Urn: ENOSPC) and no CAP_NET_RAW (AF_PACKET: EPERM), so no veth pair can be made "
                     "there (scripts/netns_gpu_probe.py, DESIGN.md)"}
@@ -944,14 +945,16 @@ def main():
     ap.add_argument("--workload", choices=["hf", "br", "br-host", "loop"], default="hf",
                     help="hf: hop-field verify on 64 B records (configs 2/3, the headline); br: config 4; "
                          "br-host: config 5 router leg; loop: config 5 RX ring -> router -> TX loop")
-    ap.add_argument("--loop-n", type=int, default=1 << 23, help="config-5 loop frames (0 = skip the leg)")
+    ap.add_argument("--loop-n", type=int, default=1 << 24, help="config-5 loop frames (0 = skip the leg)")
     ap.add_argument("--loop-chunk", type=int, default=1 << 16, help="config-5 loop frames per chunk")
     ap.add_argument("--loop-chunks", type=int, default=12, help="config-5 loop ring chunks")
-    ap.add_argument("--loop-threads", type=int, default=4, help="config-5 loop producer threads")
-    ap.add_argument("--loop-consumers", type=int, default=2, help="config-5 loop consumer threads")
+    ap.add_argument("--loop-threads", type=int, default=8, help="config-5 loop producer threads")
+    ap.add_argument("--loop-consumers", type=int, default=4, help="config-5 loop consumer threads")
     ap.add_argument("--loop-slot", type=int, default=144, help="config-5 loop ring slot bytes")
-    ap.add_argument("--loop-inflight", type=int, default=3, help="config-5 loop chunks on the GPU at once")
-    ap.add_argument("--loop-dma", action="store_true", help="config-5 loop: chunks through HBM by DMA, not zero-copy")
+    ap.add_argument("--loop-inflight", type=int, default=2, help="config-5 loop chunks on the GPU at once")
+    ap.add_argument("--loop-dma", type=int, default=2, choices=(0, 1, 2),
+                    help="config-5 loop router I/O: 0 zero-copy over PCIe, 1 DMA through HBM both ways, "
+                         "2 DMA in + the kernel writing its changes into the ring")
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--settle-s", type=float, default=0.5, help="idle seconds before each extra leg (untimed)")

@@ -393,7 +393,9 @@ struct hfv_loop_config {
     int digest;                  /* 1: sum a 64-bit digest of every transmitted frame + egress */
     int inflight;                /* chunks on the GPU at once, each on its own stream (0: 2) */
     int dma;                     /* 0: the kernel reads/writes the ring over PCIe (zero-copy);
-                                    1: each chunk is copied to HBM and back by the DMA engines */
+                                    1: each chunk is copied to HBM and back by the DMA engines;
+                                    2: copied to HBM by DMA, the kernel writes the bytes it changes
+                                       and its outputs straight back into the ring */
     uint64_t *stats;             /* nullable: per-ifindex verdict counters (added to), as hfv_br_process_host */
 };
 struct hfv_loop_stats {

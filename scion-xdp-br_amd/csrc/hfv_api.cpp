@@ -1198,7 +1198,8 @@ void hfv::forget_stream(hfv_ctx *ctx, void *stream)
 }
 
 int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen,
-                       const uint32_t *difx, size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats)
+                       const uint32_t *difx, size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats,
+                       uint8_t *dout)
 {
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
@@ -1206,7 +1207,7 @@ int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
     int e = launch_br_process(ctx->geom, ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
-                              degr, dstats, st);
+                              degr, dstats, st, nullptr, nullptr, dout);
     return after_launch(ctx, st, e, "br_process launch");
 }
 

@@ -75,7 +75,8 @@ __device__ __forceinline__ uint32_t sw32(uint32_t v) { return __builtin_bswap32(
 
 // Per-frame state: struct headers + the per-CPU scratchpad (common.h:154-225), zeroed per frame.
 struct BrFrame {
-    uint8_t *p;
+    const uint8_t *p;   // the frame as received (reads past the window)
+    uint8_t *po;        // where its changed bytes go (p itself, or the caller's output copy)
     uint32_t row;      // dword index of this frame's staged header row in s_hdr
     int win;           // staged bytes (0: read and write everything in HBM)
     uint32_t dirty;    // 16-byte chunks of the staged row written (only those go back to HBM)
@@ -138,7 +139,7 @@ __device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
         reinterpret_cast<uint8_t *>(s_hdr + k.row)[off] = (uint8_t)v;
         k.dirty |= 1u << (off >> 4);
     } else {
-        k.p[off] = (uint8_t)v;
+        k.po[off] = (uint8_t)v;
     }
 }
 __device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
@@ -148,7 +149,7 @@ __device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
         k.dirty |= (1u << (off >> 4)) | (1u << ((off + 1) >> 4));
     } else if (off >= k.win) {
-        k.p[off] = (uint8_t)v; k.p[off + 1] = (uint8_t)(v >> 8);
+        k.po[off] = (uint8_t)v; k.po[off + 1] = (uint8_t)(v >> 8);
     } else {
         wr8(k, off, v);
         wr8(k, off + 1, v >> 8);
@@ -161,7 +162,7 @@ __device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
         k.dirty |= (1u << (off >> 4)) | (1u << ((off + 3) >> 4));
     } else if (off >= k.win) {
-        uint8_t *q = k.p + off;
+        uint8_t *q = k.po + off;
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
     } else {
         wr16(k, off, v);
@@ -684,7 +685,8 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
 // there, and the next tile's bytes are already in flight while this one is parsed.
 template <int BLOCK, bool STATS, int WIN>
 __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st,
-                                                      const uint32_t *__restrict__ ttab_img, uint8_t *pkts,
+                                                      const uint32_t *__restrict__ ttab_img, const uint8_t *pkts,
+                                                      uint8_t *out,
                                                       uint64_t slot, uint32_t maxlen, uint32_t window,
                                                       const uint16_t *__restrict__ lens,
                                                       const uint32_t *__restrict__ ifidx, uint64_t n,
@@ -748,6 +750,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         if (i < n) {
             BrFrame k = {};
             k.p = pkts + i * slot;
+            k.po = out + i * slot;
             k.win = WIN;
             k.row = (wib * 64 + lane) * kBrRow;
             k.len = (int)(len <= maxlen ? len : maxlen);
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
                 uint32_t fr = r * (64 / C) + fr_of;
                 if ((cmask[r] >> ch) & 1u) {
                     const uint32_t *q = rows + fr * kBrRow + 4 * ch;
-                    *reinterpret_cast<uint4 *>(pkts + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
+                    *reinterpret_cast<uint4 *>(out + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
                 }
             }
         }
@@ -794,14 +797,21 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
-                      void *ev_start, void *ev_stop)
+                      void *ev_start, void *ev_stop, uint8_t *out)
 {
+    // `out` (default: in place) receives only the bytes the router changes; the caller keeps the
+    // rest of each frame there.  No byte is read after the router wrote it (the macinput bytes a
+    // SegID store can overwrite are kept before it, keep_mac_bytes), so reading `pkts` while
+    // writing `out` gives the in-place result.
+    if (!out) out = pkts;
     // Staged variant when the 16-byte header loads are aligned and in bounds (HFV_BR_STAGE=0
     // forces the direct one).  Persistent grid: one block per CU (LDS: tables + counters
     // [+ header rows]).
     static const int stage_env = getenv("HFV_BR_STAGE") ? atoi(getenv("HFV_BR_STAGE")) : 1;
-    bool staged = stage_env && slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0;
-    using K = void (*)(const DevState *, const uint32_t *, uint8_t *, uint64_t, uint32_t, uint32_t, const uint16_t *,
+    bool staged = stage_env && slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0 &&
+                  ((uintptr_t)out & 15) == 0;
+    using K = void (*)(const DevState *, const uint32_t *, const uint8_t *, uint8_t *, uint64_t, uint32_t, uint32_t,
+                       const uint16_t *,
                        const uint32_t *, uint64_t, uint8_t *, uint8_t *, int32_t *, unsigned long long *);
     K k;
     int block;
@@ -816,7 +826,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     uint64_t cap = (uint64_t)g.num_cus;
     unsigned grid = (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, pkts, (uint64_t)slot, maxlen,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
                           (unsigned long long *)stats);
     return (int)hipGetLastError();

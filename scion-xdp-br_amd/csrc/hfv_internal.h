@@ -170,7 +170,7 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
-                      void *ev_start = nullptr, void *ev_stop = nullptr);
+                      void *ev_start = nullptr, void *ev_stop = nullptr, uint8_t *out = nullptr);
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);
@@ -188,10 +188,11 @@ uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8])
 // and makes the ctx's device current; br_dev_launch enqueues hfv_br_process on `stream` (any
 // stream of the ctx's device) without waiting, over device-addressable frames and metadata
 // (HBM, or the device view of mapped host memory), adding the verdict counters to the device
-// array dstats (nullable).
+// array dstats (nullable).  dout (nullable: in place) receives the changed bytes of each frame
+// and must already hold the rest of it (the host ring a DMA copy came from).
 int br_zc_prepare(hfv_ctx *ctx);
 int br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen, const uint32_t *difx,
-                  size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats);
+                  size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats, uint8_t *dout = nullptr);
 // Before destroying a stream that launched with the ctx's tables (after synchronizing it):
 // drop it from the table readers the next publish would fence on.
 void forget_stream(hfv_ctx *ctx, void *stream);

@@ -105,15 +105,16 @@ using namespace hfv;
 extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struct hfv_loop_stats *out)
 {
     if (!ctx || !c || !out || !c->frames || !c->lens || c->n_frames == 0) return fail(-EINVAL, "null argument");
-    if (c->slot < 128 || (c->slot & 15) || c->chunk == 0 || c->chunks < 2 || c->total == 0)
-        return fail(-EINVAL, "slot must be a multiple of 16 and >= 128, chunk > 0, chunks >= 2, total > 0");
+    if (c->slot < 128 || (c->slot & 15) || c->chunk == 0 || c->chunks < 2 || c->total == 0 || c->dma < 0 || c->dma > 2)
+        return fail(-EINVAL, "slot must be a multiple of 16 and >= 128, chunk > 0, chunks >= 2, total > 0, dma 0..2");
     for (size_t i = 0; i < c->n_frames; ++i)
         if (c->lens[i] > c->slot || c->lens[i] > c->frame_stride) return fail(-EINVAL, "frame %zu longer than its slot", i);
     memset(out, 0, sizeof *out);
     const size_t nslots = c->chunk * c->chunks;
     const int producers = c->producers > 0 ? c->producers : 1, consumers = c->consumers > 0 ? c->consumers : 1;
     // the RX ring and the per-frame metadata in pinned, mapped host memory: the kernel reads
-    // and writes them in place (zero-copy), or the DMA engines copy them (dma = 1)
+    // and writes them in place (zero-copy), or the DMA engines copy them (dma = 1: both ways;
+    // dma = 2: in only, the kernel writing its changes back into the ring)
     int rc = br_zc_prepare(ctx);   // stops a running service; the ctx's device is current
     if (rc) return rc;
     const size_t ring_bytes = (nslots * c->slot + 4095) & ~(size_t)4095;
@@ -197,10 +198,6 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             cc.state.store(3 * (k + c->chunks), std::memory_order_release);
         }
     };
-    std::vector<std::thread> th;
-    const double t0 = now_s();
-    for (int p = 0; p < producers; ++p) th.emplace_back(produce, p);
-    for (int q = 0; q < consumers; ++q) th.emplace_back(consume, q);
     // the GPU stage: the router over each filled chunk, in ring order, `inflight` chunks at once
     // on their own streams (a chunk is a few hundred microseconds of PCIe-bound kernel; the
     // launch and completion wait of one overlap the others)
@@ -221,6 +218,11 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     if (!rc && c->stats && (hipMalloc((void **)&dstats, stats_bytes) != hipSuccess ||
                             hipMemset(dstats, 0, stats_bytes) != hipSuccess))
         rc = fail(-ENOMEM, "loop: device counters");
+    // streams, events and device buffers before the clock starts; the threads only when they are there
+    std::vector<std::thread> th;
+    const double t0 = now_s();
+    for (int p = 0; p < producers && !rc; ++p) th.emplace_back(produce, p);
+    for (int q = 0; q < consumers && !rc; ++q) th.emplace_back(consume, q);
     double gpu_busy = 0, gpu_wait = 0;
     uint64_t launched = 0, retired = 0;
     // hand finished chunks to the consumers, in order: one (waiting for it) or all that are done
@@ -252,7 +254,7 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             uint8_t *dfr_zc = dring + sl * C * c->slot, *dm = dmeta + sl * C * 16;
             rc = br_dev_launch(ctx, ss[q], dfr_zc, c->slot, (uint16_t *)dm, (uint32_t *)(dm + C * 4), cc.n, dm + C * 12,
                                dm + C * 13, (int32_t *)(dm + C * 8), dstats);
-        } else {   // frames and inputs in by DMA, the router in HBM, frames and outputs back by DMA
+        } else if (c->dma == 1) {   // frames and inputs in by DMA, the router in HBM, frames and outputs back by DMA
             uint8_t *m = dmt[q];
             if (hipMemcpyAsync(dfr[q], fr, cc.n * c->slot, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
                 hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess)
@@ -263,6 +265,15 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             if (!rc && (hipMemcpyAsync(fr, dfr[q], cc.n * c->slot, hipMemcpyDeviceToHost, ss[q]) != hipSuccess ||
                         hipMemcpyAsync(cm + C * 8, m + C * 8, C * 6, hipMemcpyDeviceToHost, ss[q]) != hipSuccess))
                 rc = fail(-EIO, "loop: D2H copy");
+        } else {   // frames and inputs in by DMA; the router reads HBM and writes only the bytes it
+                   // changes, and its outputs, straight into the mapped ring (no copy back)
+            uint8_t *m = dmt[q], *dfr_zc = dring + sl * C * c->slot, *dm = dmeta + sl * C * 16;
+            if (hipMemcpyAsync(dfr[q], fr, cc.n * c->slot, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
+                hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess)
+                rc = fail(-EIO, "loop: H2D copy");
+            if (!rc)
+                rc = br_dev_launch(ctx, ss[q], dfr[q], c->slot, (uint16_t *)m, (uint32_t *)(m + C * 4), cc.n, dm + C * 12,
+                                   dm + C * 13, (int32_t *)(dm + C * 8), dstats, dfr_zc);
         }
         if (!rc && hipEventRecord(ev[q], ss[q]) != hipSuccess) rc = fail(-EIO, "loop: event record failed");
         if (!rc) ++launched;

@@ -374,16 +374,18 @@ class Ctx:
                                          _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats)))
 
     def loop_run(self, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
-                 consumers=2, digest=False, stats=None, inflight=2, dma=False):
+                 consumers=2, digest=False, stats=None, inflight=2, dma=0):
         """Config 5 in one process (hfv_loop_run): `frames` (n x stride uint8) cycled into a
-        registered RX ring, the router over each chunk, TX/drop consumers.  Returns a dict."""
+        registered RX ring, the router over each chunk, TX/drop consumers.  dma: 0 zero-copy,
+        1 (or True) copies both ways, 2 copies in and the kernel writes its changes back.
+        Returns a dict."""
         import numpy as np
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         cfg = LoopConfig(frames=frames.ctypes.data, lens=lens.ctypes.data, n_frames=frames.shape[0],
                          frame_stride=frames.shape[1], rx_ifindex=rx_ifindex, slot=slot, chunk=chunk,
                          chunks=chunks, total=total, producers=producers, consumers=consumers,
-                         digest=1 if digest else 0, inflight=inflight, dma=1 if dma else 0, stats=_ptr(stats))
+                         digest=1 if digest else 0, inflight=inflight, dma=int(dma), stats=_ptr(stats))
         st = LoopStats()
         _check(lib().hfv_loop_run(self._h, ctypes.byref(cfg), ctypes.byref(st)))
         return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,

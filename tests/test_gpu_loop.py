@@ -42,7 +42,7 @@ def _oracle(frames, total, hf_check=True):
             "drop": int(reps[~tx].sum()), "tx_digest": digest, "verdicts": [int(x) for x in verdicts]}
 
 
-@pytest.mark.parametrize("dma", [False, True], ids=["zero_copy", "dma"])
+@pytest.mark.parametrize("dma", [0, 1, 2], ids=["zero_copy", "dma", "dma_in_zc_out"])
 @pytest.mark.parametrize("hf_check", [True, False], ids=["hf_check", "hf_check_off"])
 def test_loop_matches_oracle(gpu_ctx, hf_check, dma):
     frames = _frame_mix(97, bad_every=5)
@@ -83,14 +83,14 @@ def test_loop_single_producer_ragged_tail(gpu_ctx):
 
 def test_loop_rejects_bad_geometry(gpu_ctx):
     frames = _frame_mix(2)
-    for kw in ({"slot": 136}, {"slot": 112}, {"slot": 128}, {"chunks": 1}, {"chunk": 0}):
+    for kw in ({"slot": 136}, {"slot": 112}, {"slot": 128}, {"chunks": 1}, {"chunk": 0}, {"dma": 3}, {"dma": -1}):
         args = dict(rx_ifindex=E.RX_IFINDEX, slot=SLOT, chunk=16, chunks=2)
         args.update(kw)
         with pytest.raises(hfv.HfvError):
             gpu_ctx.loop_run(frames, np.full(2, E.FRAME_LEN), 10, **args)
 
 
-@pytest.mark.parametrize("dma", [False, True], ids=["zero_copy", "dma"])
+@pytest.mark.parametrize("dma", [0, 1, 2], ids=["zero_copy", "dma", "dma_in_zc_out"])
 def test_loop_ptf_mix_ipv4_ipv6(gpu_ctx, dma):
     """The loop over the config-4 frame mix (the reference test topology's BR 1: IPv4 and IPv6
     underlays, AS ingress, sibling hand-over, segment switch, corrupted MACs), frames of mixed

@@ -36,8 +36,8 @@ static __shared__ uint32_t s_tab128[32768];
 #define HFV_TAB3_COPIES 16
 #endif
 constexpr uint32_t kTab3Copies = HFV_TAB3_COPIES;
-constexpr uint32_t kTab3Log = kTab3Copies == 16 ? 4 : kTab3Copies == 8 ? 3 : kTab3Copies == 4 ? 2 : 99;
-static_assert(kTab3Log < 8, "HFV_TAB3_COPIES must be 4, 8 or 16");
+constexpr uint32_t kTab3Log = kTab3Copies == 32 ? 5 : kTab3Copies == 16 ? 4 : kTab3Copies == 8 ? 3 : kTab3Copies == 4 ? 2 : 99;
+static_assert(kTab3Log < 8, "HFV_TAB3_COPIES must be 4, 8, 16 or 32");
 static __shared__ uint32_t s_tab32[256 * 2 * kTab3Copies];
 static __shared__ uint4 s_keys[kDevKeyRows * HFV_MAX_KEYS];   // 48 KiB, round-major
 static __shared__ uint32_t s_valid[8];

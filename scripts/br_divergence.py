@@ -23,7 +23,26 @@ def main():
     ctx.br_set_config(TP.br_config("br1"))
     frames, ifis, good, abytes = bench.br_templates()
     tmpl, tid, lens, ifidx, _ = bench.br_batch(n, 0)
-    order = {"interleaved (bench)": np.arange(n), "sorted by template": np.argsort(tid, kind="stable")}
+    # class keys a pre-pass could compute per frame: the ingress ifindex (metadata only), + the
+    # ethertype, + the PathMeta word (CurrINF/CurrHF/SegLen: segment switch, last hop ...)
+    def meta_word(f):
+        ip = 14
+        udp = ip + (4 * (f[ip] & 15) if f[12:14] == b"\x08\x00" else 40)
+        sc = udp + 8
+        h = f[sc + 9]
+        return int.from_bytes(f[sc + 36 + 4 * ((h >> 2) & 2) + 4 * ((h >> 6) & 2):][:4], "big") if len(f) > sc + 48 else 0
+    t_if = np.array(ifis, dtype=np.int64)
+    t_eth = np.array([int.from_bytes(f[12:14], "big") for f in frames], dtype=np.int64)
+    t_meta = np.array([meta_word(f) for f in frames], dtype=np.int64)
+    k_if = t_if[tid]
+    k_if_eth = k_if * 65536 + t_eth[tid]
+    k_if_meta = (k_if << 32) + t_meta[tid]
+    order = {"interleaved (bench)": np.arange(n), "sorted by template": np.argsort(tid, kind="stable"),
+             "sorted by ifindex": np.argsort(k_if, kind="stable"),
+             "sorted by ifindex, ethertype": np.argsort(k_if_eth, kind="stable"),
+             "sorted by ifindex, PathMeta": np.argsort(k_if_meta, kind="stable")}
+    print("templates", len(frames), "ifindex classes", len(set(ifis)), "ifindex+PathMeta classes",
+          len(set(zip(t_if.tolist(), t_meta.tolist()))), flush=True)
     d_tmpl = torch.from_numpy(tmpl).cuda()
     ifis = np.array(ifis, dtype=np.int32)
     shapes = []

@@ -12,9 +12,9 @@
 // with the reference's quirks kept (listed in oracle/hfv_br_oracle.c, the CPU checker).
 // bpf_fib_lookup is replaced by the static next-hop table of the installed hfv_br_config.
 //
-// Mapping: one lane per frame, a persistent grid with one block per CU (768 threads when the
-// headers are staged, 1024 otherwise).  Each block builds the AES round tables in LDS (T0/T1,
-// 16 replicas, 32 KiB: AES is a small part of the router's work, so LDS goes to header rows),
+// Mapping: one lane per frame, a persistent grid with one block per CU (1024 threads = 16 waves).
+// Each block builds the AES round tables in LDS (T0/T1, 4 lane replicas, 8 KiB: AES is a small
+// part of the router's work, so LDS goes to header rows),
 // and stages the router tables (~10 KiB), its verdict counters (11 KiB) and, in the staged
 // variant, the first 128 bytes of each frame of its waves' tiles.  Frames are patched in place
 // in HBM through byte stores of just the header fields the rewrite touches; payload bytes are
@@ -25,10 +25,11 @@
 #include <hip/hip_ext.h>
 #include <stdlib.h>
 
-// Staging waves per CU: 12 (AES tables with 16 lane copies) or 16 (4 copies, to fit the
-// 16 header-row buffers in LDS; VGPRs then capped at 128).
+// Staging waves per CU: 16 (AES tables with 4 lane copies, to fit the 16 header-row buffers in
+// LDS; VGPRs capped at 128, which the frame state fits since the rewrite reads its inputs from
+// the staged row and the tables: 124, no scratch) or 12 (16 copies; 14 % slower).
 #ifndef HFV_BR_WAVES
-#define HFV_BR_WAVES 12
+#define HFV_BR_WAVES 16
 #endif
 #ifndef HFV_TAB3_COPIES
 #if HFV_BR_WAVES == 16
@@ -89,14 +90,15 @@ struct BrFrame {
     int ip, udp, meta, inf, hf;
     uint32_t verdict;
     uint32_t family;
-    uint32_t v4_dst, v4_src, v4_ttl;
-    uint32_t v6_dst[4], v6_src[4], v6_hop;
-    uint32_t udp_dst, udp_src;
-    uint32_t path_type, h_meta, curr_inf, curr_hf;
+    uint32_t h_meta, curr_inf, curr_hf;
     uint32_t seg_id0, seg_id1;
     uint32_t segment_switch, seg0, num_inf, num_hf;
-    uint64_t ip_residual, udp_residual;
-    uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;
+    // The next hop, as table indices: the rewrite reads the new addresses, ports and MACs from
+    // the LDS tables and the original header fields (and so the checksum residuals of
+    // rewrite.h) from the staged row, instead of the frame carrying ~20 registers of them from
+    // the parse to the rewrite.  nh: 0 IP forward (fib_lookup_ip), 1 external link, 2 sibling.
+    uint32_t nh;
+    int fwd, sib_if, route;
     int egress_ifindex;
     // deferred MAC check: ingress (mask bit 0) and egress-from-internal (bit 1) never both apply
     bool need_mac;
@@ -207,13 +209,6 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
         off += 20;
         if (beyond(k, off)) return -1;
         k.family = HFV_AF_INET;
-        k.v4_dst = rd32(k, k.ip + 16);
-        k.ip_residual -= k.v4_dst;
-        k.v4_src = rd32(k, k.ip + 12);
-        k.ip_residual -= k.v4_src;
-        k.udp_residual = k.ip_residual;
-        k.v4_ttl = rd8(k, k.ip + 8);
-        k.ip_residual -= k.v4_ttl;
         int skip = 4 * (int)(rd8(k, k.ip) & 0x0fu) - 20;
         if (skip < 0 || skip > 40) return -1;
         off += skip;
@@ -223,14 +218,6 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
         off += 40;
         if (beyond(k, off)) return -1;
         k.family = HFV_AF_INET6;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            k.v6_dst[i] = rd32(k, k.ip + 24 + 4 * i);
-            k.udp_residual -= k.v6_dst[i];
-            k.v6_src[i] = rd32(k, k.ip + 8 + 4 * i);
-            k.udp_residual -= k.v6_src[i];
-        }
-        k.v6_hop = rd8(k, k.ip + 7);
         if (rd8(k, k.ip + 6) != 17u) return -1;
     } else {
         return -1;
@@ -238,10 +225,6 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
     k.udp = off;
     off += 8;
     if (beyond(k, off)) return -1;
-    k.udp_dst = rd16(k, k.udp + 2);
-    k.udp_residual -= k.udp_dst;
-    k.udp_src = rd16(k, k.udp);
-    k.udp_residual -= k.udp_src;
     return off;
 }
 
@@ -251,9 +234,7 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     k.meta = off;
     off += 4;
     if (beyond(k, off)) return -1;
-    uint32_t raw = rd32(k, k.meta);
-    k.udp_residual -= raw;
-    k.h_meta = sw32(raw);
+    k.h_meta = sw32(rd32(k, k.meta));
     k.seg0 = (k.h_meta >> 12) & 0x3fu;
     uint32_t seg1 = (k.h_meta >> 6) & 0x3fu, seg2 = k.h_meta & 0x3fu;
     k.num_inf = (k.seg0 > 0) + (seg1 > 0) + (seg2 > 0);
@@ -264,7 +245,6 @@ __device__ __forceinline__ int parse_scion_path(BrFrame &k, int off)
     k.inf = inf;
     if (beyond(k, inf + 8)) return -1;
     k.seg_id0 = rd16(k, inf + 2);
-    k.udp_residual -= k.seg_id0;
     if (k.curr_inf + 1 < k.num_inf) {
         inf += 8;
         if (beyond(k, inf + 8)) return -1;
@@ -288,8 +268,7 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
     uint32_t haddr = rd8(k, sc + 9);
     off += 8 + 4 * (int)((haddr >> 2) & 0x2u) + 4 * (int)((haddr >> 6) & 0x2u);   // SC_GET_DL/SL, scion.h:49-52
     if (beyond(k, off)) return -1;
-    k.path_type = rd8(k, sc + 8);
-    if (k.path_type == 1u) return parse_scion_path(k, off);
+    if (rd8(k, sc + 8) == 1u) return parse_scion_path(k, off);   // path_type SCION
     k.verdict = V_NOT_IMPLEMENTED;
     return -1;
 }
@@ -375,26 +354,42 @@ __device__ __forceinline__ int int_iface(uint32_t ifindex)
     return -1;
 }
 
-__device__ __forceinline__ bool ingress_match(const DevBrIngress &e, const BrFrame &k)
+// The frame's destination as the ingress_map key holds it (common.h:94-103): the IPv4 address
+// with the IPv6 words zero, or the IPv6 words with the IPv4 address zero; and its UDP port.
+struct DstKey {
+    uint32_t v4, v6[4], port;
+};
+__device__ __forceinline__ DstKey dst_key(const BrFrame &k)
 {
-    return e.v4 == k.v4_dst && e.v6[0] == k.v6_dst[0] && e.v6[1] == k.v6_dst[1] && e.v6[2] == k.v6_dst[2] &&
-           e.v6[3] == k.v6_dst[3] && e.port == k.udp_dst && e.ifindex16 == (k.ifindex & 0xffffu);
+    DstKey d = {};
+    if (k.family == HFV_AF_INET) {
+        d.v4 = rd32(k, k.ip + 16);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d.v6[i] = rd32(k, k.ip + 24 + 4 * i);
+    }
+    d.port = rd16(k, k.udp + 2);
+    return d;
+}
+
+__device__ __forceinline__ bool ingress_match(const DevBrIngress &e, const DstKey &d, uint32_t ifindex)
+{
+    return e.v4 == d.v4 && e.v6[0] == d.v6[0] && e.v6[1] == d.v6[1] && e.v6[2] == d.v6[2] && e.v6[3] == d.v6[3] &&
+           e.port == d.port && e.ifindex16 == (ifindex & 0xffffu);
 }
 
 __device__ __forceinline__ int ingress_lookup(const BrFrame &k)
 {
     const uint32_t x = k.ifindex & 0xffffu;
+    int c = -2;
     if (x < 64) {   // the only entry on this interface, if there is just one
-        const int c = s_br.ing_of_ifindex[x];
+        c = s_br.ing_of_ifindex[x];
         if (c == -1) return -1;
-        if (c >= 0) return ingress_match(s_br.ingress[c], k) ? c : -1;
     }
-    for (uint32_t i = 0; i < s_br.n_ing; ++i) {
-        const DevBrIngress &e = s_br.ingress[i];
-        if (e.v4 == k.v4_dst && e.v6[0] == k.v6_dst[0] && e.v6[1] == k.v6_dst[1] && e.v6[2] == k.v6_dst[2] &&
-            e.v6[3] == k.v6_dst[3] && e.port == k.udp_dst && e.ifindex16 == (k.ifindex & 0xffffu))
-            return (int)i;
-    }
+    const DstKey d = dst_key(k);
+    if (c >= 0) return ingress_match(s_br.ingress[c], d, k.ifindex) ? c : -1;
+    for (uint32_t i = 0; i < s_br.n_ing; ++i)
+        if (ingress_match(s_br.ingress[i], d, k.ifindex)) return (int)i;
     return -1;
 }
 
@@ -424,7 +419,8 @@ __device__ __forceinline__ int route_lookup(uint32_t family, uint32_t d0, uint32
     return best;
 }
 
-// bpf_fib_lookup return-code handling shared by the fib_lookup_* helpers; false = stop
+// bpf_fib_lookup return-code handling shared by the fib_lookup_* helpers; false = stop.  The
+// route's MAC addresses are read by the rewrite (k.route).
 __device__ __forceinline__ bool fib_result(BrFrame &k, int r)
 {
     int ret = r >= 0 ? s_br.routes[r].ret : 4;   // no route: BPF_FIB_LKUP_RET_NOT_FWDED
@@ -436,41 +432,16 @@ __device__ __forceinline__ bool fib_result(BrFrame &k, int r)
         k.verdict = V_FIB_PASS;
         return false;
     }
-    if (r >= 0) {
-        const DevBrRoute &e = s_br.routes[r];
-        k.dmac_lo = e.dmac_lo; k.dmac_hi = e.dmac_hi;
-        k.smac_lo = e.smac_lo; k.smac_hi = e.smac_hi;
-    } else {
-        k.dmac_lo = k.dmac_hi = k.smac_lo = k.smac_hi = 0;
-    }
+    k.route = r;
     return true;
-}
-
-// The family-dependent field updates below are written as selects, not branches: LLVM would
-// otherwise sink the v4 and v6 stores into one store through a pointer phi and keep the
-// frame's address fields in scratch.
-__device__ __forceinline__ void set_dst(BrFrame &k, const uint32_t a[4])
-{
-    const bool v4 = k.family == HFV_AF_INET;
-    k.v4_dst = v4 ? a[0] : k.v4_dst;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) k.v6_dst[i] = v4 ? k.v6_dst[i] : a[i];
-}
-__device__ __forceinline__ void set_src(BrFrame &k, const uint32_t a[4])
-{
-    const bool v4 = k.family == HFV_AF_INET;
-    k.v4_src = v4 ? a[0] : k.v4_src;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) k.v6_src[i] = v4 ? k.v6_src[i] : a[i];
-    k.v4_ttl = v4 ? 64u : k.v4_ttl;
-    k.v6_hop = v4 ? k.v6_hop : 64u;
 }
 
 // fib_lookup_ip's route: hdr->ip.v4->daddr or the IPv6 destination
 __device__ __forceinline__ int ip_route(const BrFrame &k)
 {
     if (k.family == HFV_AF_INET) return route_lookup(k.family, sw32(rd32(k, k.ip + 16)), 0, 0, 0);
-    return route_lookup(k.family, sw32(k.v6_dst[0]), sw32(k.v6_dst[1]), sw32(k.v6_dst[2]), sw32(k.v6_dst[3]));
+    return route_lookup(k.family, sw32(rd32(k, k.ip + 24)), sw32(rd32(k, k.ip + 28)), sw32(rd32(k, k.ip + 32)),
+                        sw32(rd32(k, k.ip + 36)));
 }
 
 // ---- rewrite.h -------------------------------------------------------------------------------
@@ -483,52 +454,87 @@ __device__ __forceinline__ uint32_t fold_checksum(uint64_t c)
     return (uint32_t)(c & 0xffffu);
 }
 
+// rewrite / rewrite_scion_path (rewrite.h:35-146).  The BPF code subtracts every original
+// field from its u64 checksum residuals as it parses them and adds the new values here; the
+// residuals are sums mod 2^64, so taking the originals from the staged row (nothing is written
+// before they are read) and both sums here gives the same residuals.  New values: the route's
+// MACs; for a link (nh 1) or a sibling (nh 2) the link's remote address and port as the
+// destination and the link's local (or the sibling's internal interface's) address and port
+// as the source with TTL / hop limit 64; for an IP forward (nh 0) the original addresses and
+// ports and the IPv4 TTL decremented.
 __device__ __forceinline__ void rewrite(BrFrame &k)
 {
-    wr32(k, 0, k.dmac_lo); wr16(k, 4, k.dmac_hi);
-    wr32(k, 6, k.smac_lo); wr16(k, 10, k.smac_hi);
+    const bool fw = k.nh != 0;
+    const DevBrEgress &e = s_br.egress[fw ? k.fwd : 0];
+    const DevBrIntIface &si = s_br.int_ifaces[k.nh == 2 ? k.sib_if : 0];
+    const bool sib = k.nh == 2;
+    const uint32_t od_port = rd16(k, k.udp + 2), os_port = rd16(k, k.udp);
+    const uint32_t o_seg0 = rd16(k, k.inf + 2);
+    uint64_t udp_res = 0;
+    udp_res -= (uint64_t)od_port;
+    udp_res -= (uint64_t)os_port;
+    udp_res -= (uint64_t)sw32(k.h_meta);
+    udp_res -= (uint64_t)o_seg0;
+    {
+        const DevBrRoute &rt = s_br.routes[k.route >= 0 ? k.route : 0];
+        const bool ok = k.route >= 0;
+        wr32(k, 0, ok ? rt.dmac_lo : 0u); wr16(k, 4, ok ? rt.dmac_hi : 0u);
+        wr32(k, 6, ok ? rt.smac_lo : 0u); wr16(k, 10, ok ? rt.smac_hi : 0u);
+    }
     if (k.family == HFV_AF_INET) {
-        wr32(k, k.ip + 16, k.v4_dst);
-        wr32(k, k.ip + 12, k.v4_src);
-        uint64_t c = (uint64_t)k.v4_dst + (uint64_t)k.v4_src;
-        k.ip_residual += c;
-        k.udp_residual += c;
-        wr8(k, k.ip + 8, k.v4_ttl);
-        k.ip_residual += k.v4_ttl;
-        uint64_t cs = ~(uint64_t)rd16(k, k.ip + 10) + k.ip_residual + 1;
+        const uint32_t od = rd32(k, k.ip + 16), os = rd32(k, k.ip + 12), ottl = rd8(k, k.ip + 8);
+        const uint32_t nd = fw ? e.remote[0] : od;
+        const uint32_t ns = fw ? (sib ? si.addr[0] : e.local[0]) : os;
+        const uint32_t nttl = fw ? 64u : ((ottl - 1u) & 0xffu);
+        const uint64_t c = (uint64_t)nd + (uint64_t)ns - (uint64_t)od - (uint64_t)os;
+        wr32(k, k.ip + 16, nd);
+        wr32(k, k.ip + 12, ns);
+        udp_res += c;
+        wr8(k, k.ip + 8, nttl);
+        const uint64_t ip_res = c + (uint64_t)nttl - (uint64_t)ottl;
+        uint64_t cs = ~(uint64_t)rd16(k, k.ip + 10) + ip_res + 1;
         wr16(k, k.ip + 10, fold_checksum(cs));
     } else {
-        if (k.ip + 24 + 16 < k.len && k.ip + 8 + 16 < k.len) {
+        const bool put = k.ip + 24 + 16 < k.len && k.ip + 8 + 16 < k.len;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                wr32(k, k.ip + 24 + 4 * i, k.v6_dst[i]);
-                k.udp_residual += k.v6_dst[i];
-                wr32(k, k.ip + 8 + 4 * i, k.v6_src[i]);
-                k.udp_residual += k.v6_src[i];
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t od = rd32(k, k.ip + 24 + 4 * i), os = rd32(k, k.ip + 8 + 4 * i);
+            udp_res -= (uint64_t)od;
+            udp_res -= (uint64_t)os;
+            if (put) {
+                const uint32_t nd = fw ? e.remote[i] : od;
+                const uint32_t ns = fw ? (sib ? si.addr[i] : e.local[i]) : os;
+                wr32(k, k.ip + 24 + 4 * i, nd);
+                wr32(k, k.ip + 8 + 4 * i, ns);
+                udp_res += (uint64_t)nd;
+                udp_res += (uint64_t)ns;
             }
         }
-        wr8(k, k.ip + 7, k.v6_hop);
+        if (fw) wr8(k, k.ip + 7, 64u);
+        else wr8(k, k.ip + 7, rd8(k, k.ip + 7));   // the BPF code stores the unchanged hop limit
     }
-    wr16(k, k.udp + 2, k.udp_dst);
-    wr16(k, k.udp, k.udp_src);
-    k.udp_residual += k.udp_dst;
-    k.udp_residual += k.udp_src;
+    const uint32_t nd_port = fw ? e.remote_port : od_port;
+    const uint32_t ns_port = fw ? (sib ? si.port : e.local_port) : os_port;
+    wr16(k, k.udp + 2, nd_port);
+    wr16(k, k.udp, ns_port);
+    udp_res += (uint64_t)nd_port;
+    udp_res += (uint64_t)ns_port;
     // path_type is SCION here (the only type process_packet lets through)
     uint32_t meta = (k.h_meta & 0x00ffffffu) | ((k.curr_hf & 0x3fu) << 24) | (k.curr_inf << 30);
     wr32(k, k.meta, sw32(meta));
-    k.udp_residual += sw32(meta);
+    udp_res += (uint64_t)sw32(meta);
     int inf = k.inf;
     wr16(k, inf + 2, k.seg_id0);
-    k.udp_residual += k.seg_id0;
+    udp_res += (uint64_t)k.seg_id0;
     if (k.segment_switch) {
         inf += 8;
         if (inf + 8 <= k.len) {
-            k.udp_residual -= rd16(k, inf + 2);
-            k.udp_residual += k.seg_id1;
+            udp_res -= (uint64_t)rd16(k, inf + 2);
+            udp_res += (uint64_t)k.seg_id1;
             wr16(k, inf + 2, k.seg_id1);
         }
     }
-    uint64_t cs = ~(uint64_t)rd16(k, k.udp + 6) + k.udp_residual + 1;
+    uint64_t cs = ~(uint64_t)rd16(k, k.udp + 6) + udp_res + 1;
     wr16(k, k.udp + 6, fold_checksum(cs));
 }
 
@@ -595,30 +601,20 @@ __device__ __forceinline__ int process_packet(BrFrame &k)
     int r;
     if (ext || sib) {
         if (fwd.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
-        k.udp_dst = fwd.remote_port;
-        set_dst(k, fwd.remote);
         r = fwd.route;   // route_lookup of the link's remote address, resolved with the tables
     } else {
         r = ip_route(k);
     }
     if (!fib_result(k, r)) return (int)record<STATS>(k, k.verdict);
     const int egress = r >= 0 ? (int)s_br.routes[r].ifindex : 0;
-    if (ext || sib) {
-        const uint32_t *src_addr = fwd.local;
-        uint32_t src_port = fwd.local_port;
-        if (sib) {   // the sibling's packets leave from the internal interface on the route
-            const int s = fwd.sib_iface;   // int_iface(egress)
-            if (s < 0) return (int)record<STATS>(k, V_ABORT);
-            const DevBrIntIface &src = s_br.int_ifaces[s];
-            if (src.family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
-            src_addr = src.addr;
-            src_port = src.port;
-        }
-        k.udp_src = src_port;
-        set_src(k, src_addr);
-    } else {
-        k.v4_ttl = (k.v4_ttl - 1u) & 0xffu;
+    if (sib) {   // the sibling's packets leave from the internal interface on the route
+        const int s = fwd.sib_iface;   // int_iface(egress)
+        if (s < 0) return (int)record<STATS>(k, V_ABORT);
+        if (s_br.int_ifaces[s].family != k.family) return (int)record<STATS>(k, V_UNDERLAY_MISMATCH);
     }
+    k.nh = ext ? 1u : sib ? 2u : 0u;
+    k.fwd = f;
+    k.sib_if = fwd.sib_iface;
     if (k.need_mac) keep_mac_bytes(k);
     rewrite(k);
     k.egress_ifindex = egress;
@@ -633,7 +629,7 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 
 // ---- kernel ------------------------------------------------------------------------------------
 template <bool STATS>
-__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTable *keys, const Lane &l,
+__device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTable *keys,
                                          uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
                                          int32_t *__restrict__ egress)
 {
@@ -667,6 +663,7 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
             }
             const UniformKey ukey(keys);
             uint32_t t0, t1;
+            const Lane l = lane_bases3();   // formed here: none of it stays live through the parse
             cmac48_macinput<3>(mi, ukey, l, t0, t1);
             ok = ukey.ok && t0 == mac_lo && (t1 & 0xffffu) == mac_hi;
         }
@@ -705,16 +702,17 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     if constexpr (STATS)
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) s_stats[e] = 0;
     __syncthreads();
-    const Lane l = lane_bases3();
 
     const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint64_t ntiles = (n + 63) / 64, nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
     uint64_t t = (uint64_t)blockIdx.x * (BLOCK / 64) + wib;
     const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
     // The tile's header rows and the lane's own length / ingress ifindex are loaded at the top
-    // of each tile, with no register prefetch of the next tile: the other waves of the CU (12
+    // of each tile, with no register prefetch of the next tile: the other waves of the CU (16
     // in the staged launch) hide the latency, and the prefetch's extra registers pushed the
-    // 12-wave kernel into scratch spills (measured 152 us against 121 us).
+    // 12-wave kernel into scratch spills (measured 152 us against 121 us); pulling
+    // the next tile into L2 with one dword load per frame was 8 % slower (its load sits in the
+    // in-order vmcnt queue of the current tile, profiles/r02/br_ab/pf_lane_w16_ab_r02c1.log).
     uint4 pre[C];
     uint32_t pre_len = 0, pre_ifx = 0;
     auto fetch = [&](uint64_t tt) {
@@ -756,7 +754,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             k.len = (int)(len <= maxlen ? len : maxlen);
             k.lim = k.len < (int)window ? k.len : (int)window;
             k.ifindex = ifx;
-            br_frame<STATS>(k, i, &st->keys, l, action, verdict, egress);
+            br_frame<STATS>(k, i, &st->keys, action, verdict, egress);
             dirty = k.dirty;
         }
         if constexpr (WIN > 0) {

@@ -26,12 +26,13 @@ static __constant__ uint32_t c_t0[256] = {T0V64(0), T0V64(64), T0V64(128), T0V64
 // four (128 KiB) and needs no rotation.
 static __shared__ uint32_t s_tab64[16384];
 static __shared__ uint32_t s_tab128[32768];
-// TAB = 3: T0/T1 with kTab3Copies lane copies (16: 32 KiB) for kernels where AES is a small
+// TAB = 3: T0/T1 with kTab3Copies lane copies (4: 8 KiB) for kernels where AES is a small
 // part of the work and LDS is needed for other things (the router kernel): byte address
-//   (x << (3 + log2 copies)) | (t << (2 + log2 copies)) | ((L % copies) << 2)
-// formed with a shift instead of v_perm, at the cost of bank conflicts between the lanes of a
-// 32-lane half that share a copy (2-way at 16 copies).  A translation unit may define
-// HFV_TAB3_COPIES before including this header.
+//   (t << (10 + log2 copies)) | (x << (2 + log2 copies)) | ((L % copies) << 2)
+// formed with a shift instead of v_perm.  The table bit sits above the bank bits, so the
+// lanes that share a copy spread over 32 / copies banks by x (at 4 copies: 8 lanes of a
+// 32-lane half over 8 banks); lanes of one copy still conflict when their x differ in the
+// bank bits' range.  A translation unit may define HFV_TAB3_COPIES before including this header.
 #ifndef HFV_TAB3_COPIES
 #define HFV_TAB3_COPIES 16
 #endif
@@ -68,8 +69,8 @@ __device__ __forceinline__ void fill_ttab()
     if constexpr (TAB == 3) {
 #pragma unroll 4
         for (int e = threadIdx.x; e < (int)(256 * 2 * kTab3Copies); e += blockDim.x) {
-            uint32_t t = c_t0[e >> (kTab3Log + 1)];
-            s_tab32[e] = ((e >> kTab3Log) & 1) ? __builtin_amdgcn_alignbit(t, t, 24) : t;   // T1 = rotl8(T0)
+            uint32_t t = c_t0[(e >> kTab3Log) & 255];
+            s_tab32[e] = (e >> (kTab3Log + 8)) ? __builtin_amdgcn_alignbit(t, t, 24) : t;   // T1 = rotl8(T0)
         }
         return;
     }
@@ -157,7 +158,7 @@ __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l
 {
     static_assert(K >= 0 && K < 4, "state byte");
     if constexpr (TAB == 3) {
-        const uint32_t a3 = (__builtin_amdgcn_ubfe(w, 8 * K, 8) << (kTab3Log + 3)) | base;
+        const uint32_t a3 = (__builtin_amdgcn_ubfe(w, 8 * K, 8) << (kTab3Log + 2)) | base;
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab32) + a3);
     }
     const uint32_t a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
@@ -337,7 +338,7 @@ __device__ __forceinline__ Lane lane_bases3()
 {
     Lane l = lane_bases();
     l.b0 = (threadIdx.x & (kTab3Copies - 1)) << 2;
-    l.b1 = l.b0 | (1u << (kTab3Log + 2));
+    l.b1 = l.b0 | (1u << (kTab3Log + 10));
     l.b2 = l.b0;
     l.b3 = l.b1;
     return l;

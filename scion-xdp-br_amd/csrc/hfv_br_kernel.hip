@@ -705,7 +705,10 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
 
     const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const uint64_t ntiles = (n + 63) / 64, nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
-    uint64_t t = (uint64_t)blockIdx.x * (BLOCK / 64) + wib;
+    // Tiles go round the blocks first (wave w of block b starts at tile w * grid + b), so a
+    // launch of fewer tiles than waves (the config-5 loop's 64 Ki-frame chunks: 1024 tiles)
+    // still spreads over every CU instead of filling a quarter of them with 16 waves each.
+    uint64_t t = (uint64_t)wib * gridDim.x + blockIdx.x;
     const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
     // The tile's header rows and the lane's own length / ingress ifindex are loaded at the top
     // of each tile, with no register prefetch of the next tile: the other waves of the CU (16
@@ -820,9 +823,8 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
         block = 1024;
         k = stats ? k_br_process<1024, true, 0> : k_br_process<1024, false, 0>;
     }
-    uint64_t blocks = (n + block - 1) / block;
-    uint64_t cap = (uint64_t)g.num_cus;
-    unsigned grid = (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
+    const uint64_t tiles = (n + 63) / 64, cap = (uint64_t)g.num_cus;   // one block per CU at most
+    unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,

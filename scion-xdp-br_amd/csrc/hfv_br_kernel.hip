@@ -54,6 +54,32 @@ constexpr int kBrRow = kBrWin / 4 + 1;
 constexpr int kBrStageWaves = HFV_BR_WAVES;
 static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 
+// HFV_BR_PROF = 1: diagnostic build.  Each wave adds the shader cycles (s_memtime) it spends in
+// the phases of a tile into g_br_prof (read by hfv_debug_br_prof): [0] header loads issued ->
+// staged, [1] parse/process_packet, [2] MAC check + outputs, [3] write-back, [4] tiles.
+#ifndef HFV_BR_PROF
+#define HFV_BR_PROF 0
+#endif
+#if HFV_BR_PROF
+__device__ unsigned long long g_br_prof[8];
+#endif
+struct BrProf {
+    uint64_t c[5] = {0, 0, 0, 0, 0};
+    uint64_t t = 0;
+    __device__ __forceinline__ void start()
+    {
+        if constexpr (HFV_BR_PROF) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void mark(int i)
+    {
+        if constexpr (HFV_BR_PROF) {
+            const uint64_t x = __builtin_amdgcn_s_memtime();
+            c[i] += x - t;
+            t = x;
+        }
+    }
+};
+
 // enum xdp_action and enum verdict (br/src/bpf/common.h:38-70)
 enum : uint32_t { A_ABORTED = 0, A_DROP = 1, A_PASS = 2, A_TX = 3, A_REDIRECT = 4 };
 constexpr uint32_t verd(uint32_t action, uint32_t counter) { return (action & 7u) | (counter << 3); }
@@ -631,9 +657,10 @@ __device__ __forceinline__ bool tx_port(int ifindex)
 template <bool STATS>
 __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTable *keys,
                                          uint8_t *__restrict__ action, uint8_t *__restrict__ verdict,
-                                         int32_t *__restrict__ egress)
+                                         int32_t *__restrict__ egress, BrProf &prof)
 {
     int a = process_packet<STATS>(k);
+    prof.mark(1);
     if (k.cut) {   // headers reach past the window: untouched, uncounted, caller re-runs it whole
         action[i] = HFV_BR_ACTION_RETRY;
         verdict[i] = 0;
@@ -732,7 +759,9 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         pre_len = lens[fi];
         pre_ifx = ifidx[fi];
     };
+    BrProf prof;
     for (; t < ntiles; t += nwaves) {
+        prof.start();
         fetch(t);
         if constexpr (WIN > 0) {
             uint32_t *rows = s_hdr + wib * 64 * kBrRow;
@@ -746,6 +775,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         const uint32_t len = pre_len, ifx = pre_ifx;
+        if constexpr (HFV_BR_PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prof.mark(0);
         uint64_t i = t * 64 + lane;
         uint32_t dirty = 0;
         if (i < n) {
@@ -757,9 +788,10 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             k.len = (int)(len <= maxlen ? len : maxlen);
             k.lim = k.len < (int)window ? k.len : (int)window;
             k.ifindex = ifx;
-            br_frame<STATS>(k, i, &st->keys, action, verdict, egress);
+            br_frame<STATS>(k, i, &st->keys, action, verdict, egress, prof);
             dirty = k.dirty;
         }
+        prof.mark(2);
         if constexpr (WIN > 0) {
             // write the rewritten 16-byte chunks back (WIN / 16 lanes per frame, each storing its
             // chunk if the frame's lane wrote into it): untouched chunks stay clean in L2, so a
@@ -785,7 +817,14 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        if constexpr (HFV_BR_PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prof.mark(3);
+        prof.c[4] += 1;
     }
+#if HFV_BR_PROF
+    if (lane == 0)
+        for (int q = 0; q < 5; ++q) atomicAdd(&g_br_prof[q], (unsigned long long)prof.c[q]);
+#endif
     if constexpr (STATS) {
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) {
@@ -794,6 +833,16 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         }
     }
 }
+
+#if HFV_BR_PROF
+// diagnostics: the phase counters of the kernels run since the last call (then cleared)
+extern "C" int hfv_debug_br_prof(unsigned long long out[8])
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_br_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_br_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,

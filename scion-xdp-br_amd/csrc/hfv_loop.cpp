@@ -98,22 +98,6 @@ struct Chunk {
     size_t n = 0;                     // frames in it
 };
 
-// Pins the calling thread to a NUMA node for the guard's life and restores its CPU set after:
-// the ring is allocated, and the router stage runs, on the GPU's node.
-struct AffinityGuard {
-    cpu_set_t saved;
-    bool ok;
-    explicit AffinityGuard(int numa_node)
-    {
-        ok = pthread_getaffinity_np(pthread_self(), sizeof saved, &saved) == 0;
-        if (ok) pin(numa_node);
-    }
-    ~AffinityGuard()
-    {
-        if (ok) (void)pthread_setaffinity_np(pthread_self(), sizeof saved, &saved);
-    }
-};
-
 }  // namespace
 
 using namespace hfv;
@@ -133,8 +117,6 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     // dma = 2: in only, the kernel writing its changes back into the ring)
     int rc = br_zc_prepare(ctx);   // stops a running service; the ctx's device is current
     if (rc) return rc;
-    const int node = hfv_ctx_numa_node(ctx);
-    const AffinityGuard on_node(node);
     const size_t ring_bytes = (nslots * c->slot + 4095) & ~(size_t)4095;
     const size_t meta_bytes = (nslots * 16 + 4095) & ~(size_t)4095;
     uint8_t *ring = nullptr, *meta = nullptr, *dring = nullptr, *dmeta = nullptr;
@@ -155,6 +137,7 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     auto egr_of = [&](size_t s) { return (int32_t *)(meta + s * C * 16 + C * 8); };
     auto act_of = [&](size_t s) { return meta + s * C * 16 + C * 12; };
     auto ver_of = [&](size_t s) { return meta + s * C * 16 + C * 13; };
+    const int node = hfv_ctx_numa_node(ctx);
     std::vector<Chunk> ch(c->chunks);
     for (size_t i = 0; i < c->chunks; ++i) ch[i].state.store(3 * i);
     const uint64_t nchunks_total = (c->total + c->chunk - 1) / c->chunk;

@@ -136,7 +136,10 @@ struct BrFrame {
 
 // Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
 // staged window come from LDS (a 32-bit field = two aligned ds_read_b32 + v_alignbyte), the
-// rest from the frame in HBM.
+// rest from the frame in HBM.  The LDS read is unconditional (clamped into the row) and only
+// the rare read past the window is a branch: with the LDS read inside the branch, every header
+// field cost its own basic block and a full LDS round trip (s_waitcnt lgkmcnt(0) per field), so
+// nothing overlapped the parse's ~300 LDS latencies.
 __device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
 {
     const uint32_t *row = s_hdr + k.row;
@@ -145,56 +148,79 @@ __device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
 }
 __device__ __forceinline__ uint32_t rd8(const BrFrame &k, int off)
 {
-    if (off < k.win) return reinterpret_cast<const uint8_t *>(s_hdr + k.row)[off];
-    return g8(k.p + off);
+    if (k.win == 0) return g8(k.p + off);
+    const bool in = (uint32_t)off < (uint32_t)k.win;
+    uint32_t v = reinterpret_cast<const uint8_t *>(s_hdr + k.row)[in ? off : 0];
+    if (!in) v = g8(k.p + off);
+    return v;
 }
 __device__ __forceinline__ uint32_t rd16(const BrFrame &k, int off)
 {
-    if (off + 2 <= k.win) return lds_u32_at(k, off) & 0xffffu;
-    return g16(k.p + off);
+    if (k.win == 0) return g16(k.p + off);
+    const bool in = (uint32_t)off + 2 <= (uint32_t)k.win;
+    uint32_t v = lds_u32_at(k, in ? off : 0) & 0xffffu;
+    if (!in) v = g16(k.p + off);
+    return v;
 }
 __device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
 {
-    if (off + 4 <= k.win) return lds_u32_at(k, off);
-    return g32(k.p + off);
+    if (k.win == 0) return g32(k.p + off);
+    const bool in = (uint32_t)off + 4 <= (uint32_t)k.win;
+    uint32_t v = lds_u32_at(k, in ? off : 0);
+    if (!in) v = g32(k.p + off);
+    return v;
 }
 
 // Header writes: bytes inside the staged window go to the LDS row (written back to HBM with
-// coalesced 16-byte stores at the end of the tile), bytes past it straight to HBM.
+// coalesced 16-byte stores at the end of the tile), bytes past it straight to HBM.  As with the
+// reads, the LDS store is unconditional: a field not wholly inside the window is stored into
+// the row's pad dword (bytes kBrWin..kBrWin+3, never read for a result nor written back) and
+// then handled on the rare branch.
+constexpr int kBrPad = kBrWin;
+__device__ __forceinline__ uint32_t chunk_bit(int off) { return 1u << ((uint32_t)off >> 4 & 31u); }
 __device__ __forceinline__ void wr8(BrFrame &k, int off, uint32_t v)
 {
-    if (off < k.win) {
-        reinterpret_cast<uint8_t *>(s_hdr + k.row)[off] = (uint8_t)v;
-        k.dirty |= 1u << (off >> 4);
-    } else {
-        k.po[off] = (uint8_t)v;
-    }
+    if (k.win == 0) { k.po[off] = (uint8_t)v; return; }
+    const bool in = (uint32_t)off < (uint32_t)k.win;
+    reinterpret_cast<uint8_t *>(s_hdr + k.row)[in ? off : kBrPad] = (uint8_t)v;
+    k.dirty |= in ? chunk_bit(off) : 0u;
+    if (!in) k.po[off] = (uint8_t)v;
 }
 __device__ __forceinline__ void wr16(BrFrame &k, int off, uint32_t v)
 {
-    if (off + 2 <= k.win) {   // whole field in the window (the common case): one check
-        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
-        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
-        k.dirty |= (1u << (off >> 4)) | (1u << ((off + 1) >> 4));
-    } else if (off >= k.win) {
-        k.po[off] = (uint8_t)v; k.po[off + 1] = (uint8_t)(v >> 8);
-    } else {
-        wr8(k, off, v);
-        wr8(k, off + 1, v >> 8);
+    if (k.win == 0) { k.po[off] = (uint8_t)v; k.po[off + 1] = (uint8_t)(v >> 8); return; }
+    const bool in = (uint32_t)off + 2 <= (uint32_t)k.win;   // whole field in the window (the common case)
+    uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + (in ? off : kBrPad);
+    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8);
+    k.dirty |= in ? chunk_bit(off) | chunk_bit(off + 1) : 0u;
+    if (!in) {
+        if (off >= k.win) {
+            k.po[off] = (uint8_t)v; k.po[off + 1] = (uint8_t)(v >> 8);
+        } else {
+            wr8(k, off, v);
+            wr8(k, off + 1, v >> 8);
+        }
     }
 }
 __device__ __forceinline__ void wr32(BrFrame &k, int off, uint32_t v)
 {
-    if (off + 4 <= k.win) {
-        uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + off;
-        q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
-        k.dirty |= (1u << (off >> 4)) | (1u << ((off + 3) >> 4));
-    } else if (off >= k.win) {
+    if (k.win == 0) {
         uint8_t *q = k.po + off;
         q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
-    } else {
-        wr16(k, off, v);
-        wr16(k, off + 2, v >> 16);
+        return;
+    }
+    const bool in = (uint32_t)off + 4 <= (uint32_t)k.win;
+    uint8_t *q = reinterpret_cast<uint8_t *>(s_hdr + k.row) + (in ? off : kBrPad);
+    q[0] = (uint8_t)v; q[1] = (uint8_t)(v >> 8); q[2] = (uint8_t)(v >> 16); q[3] = (uint8_t)(v >> 24);
+    k.dirty |= in ? chunk_bit(off) | chunk_bit(off + 3) : 0u;
+    if (!in) {
+        if (off >= k.win) {
+            uint8_t *h = k.po + off;
+            h[0] = (uint8_t)v; h[1] = (uint8_t)(v >> 8); h[2] = (uint8_t)(v >> 16); h[3] = (uint8_t)(v >> 24);
+        } else {
+            wr16(k, off, v);
+            wr16(k, off + 2, v >> 16);
+        }
     }
 }
 

@@ -202,13 +202,22 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     // on their own streams (a chunk is a few hundred microseconds of PCIe-bound kernel; the
     // launch and completion wait of one overlap the others)
     const int D = c->inflight > 0 ? (c->inflight < (int)c->chunks ? c->inflight : (int)c->chunks) : 2;
-    std::vector<hipStream_t> ss(D, nullptr);
-    std::vector<hipEvent_t> ev(D, nullptr);
+    std::vector<hipStream_t> ss(D, nullptr), ss2(D, nullptr);
+    std::vector<hipEvent_t> ev(D, nullptr), ev2(D, nullptr);
+    // DMA in: each chunk's frame copy goes out in two halves on two streams (HIP gives each stream
+    // its own copy-engine queue, and one engine does not fill the link: with a chunk on one
+    // stream, runs landed at 166-172 or 213-265 Mpkt/s depending on the engines the streams got)
+    static const int split_env = getenv("HFV_LOOP_SPLIT") ? atoi(getenv("HFV_LOOP_SPLIT")) : 1;
+    const bool split = c->dma == 2 && split_env;
     uint64_t *dstats = nullptr;
     const size_t stats_bytes = HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8;
     for (int i = 0; i < D && !rc; ++i) {
         if (hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+            rc = fail(-EIO, "loop: stream/event creation failed");
+        if (!rc && split &&
+            (hipStreamCreateWithFlags(&ss2[i], hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreateWithFlags(&ev2[i], hipEventDisableTiming) != hipSuccess))
             rc = fail(-EIO, "loop: stream/event creation failed");
     }
     std::vector<uint8_t *> dfr(D, nullptr), dmt(D, nullptr);   // DMA variant: device twin per stream
@@ -268,8 +277,14 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         } else {   // frames and inputs in by DMA; the router reads HBM and writes only the bytes it
                    // changes, and its outputs, straight into the mapped ring (no copy back)
             uint8_t *m = dmt[q], *dfr_zc = dring + sl * C * c->slot, *dm = dmeta + sl * C * 16;
-            if (hipMemcpyAsync(dfr[q], fr, cc.n * c->slot, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
-                hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess)
+            const size_t half = split ? cc.n / 2 * c->slot : 0, all = cc.n * c->slot;
+            if (split && (hipStreamWaitEvent(ss2[q], ev[q], 0) != hipSuccess ||   // its previous kernel is done with dfr[q]
+                          hipMemcpyAsync(dfr[q] + half, fr + half, all - half, hipMemcpyHostToDevice, ss2[q]) != hipSuccess ||
+                          hipEventRecord(ev2[q], ss2[q]) != hipSuccess))
+                rc = fail(-EIO, "loop: H2D copy");
+            if (!rc && (hipMemcpyAsync(dfr[q], fr, split ? half : all, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
+                        hipMemcpyAsync(m, cm, C * 8, hipMemcpyHostToDevice, ss[q]) != hipSuccess ||
+                        (split && hipStreamWaitEvent(ss[q], ev2[q], 0) != hipSuccess)))
                 rc = fail(-EIO, "loop: H2D copy");
             if (!rc)
                 rc = br_dev_launch(ctx, ss[q], dfr[q], c->slot, (uint16_t *)m, (uint32_t *)(m + C * 4), cc.n, dm + C * 12,
@@ -311,6 +326,11 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             (void)hipStreamDestroy(ss[i]);
         }
         if (ev[i]) (void)hipEventDestroy(ev[i]);
+        if (ss2[i]) {
+            (void)hipStreamSynchronize(ss2[i]);
+            (void)hipStreamDestroy(ss2[i]);
+        }
+        if (ev2[i]) (void)hipEventDestroy(ev2[i]);
     }
     if (dstats) (void)hipFree(dstats);
     for (int i = 0; i < D; ++i) {

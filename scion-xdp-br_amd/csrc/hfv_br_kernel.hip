@@ -15,10 +15,10 @@
 // Mapping: one lane per frame, a persistent grid with one block per CU (1024 threads = 16 waves).
 // Each block builds the AES round tables in LDS (T0/T1, 4 lane replicas, 8 KiB: AES is a small
 // part of the router's work, so LDS goes to header rows),
-// and stages the router tables (~10 KiB), its verdict counters (11 KiB) and, in the staged
-// variant, the first 128 bytes of each frame of its waves' tiles.  Frames are patched in place
-// in HBM through byte stores of just the header fields the rewrite touches; payload bytes are
-// never read.  At most one hop field is checked per frame (ingress from a neighbour AS or
+// and stages the router tables (~6.5 KiB), its verdict counters (11 KiB) and, in the staged
+// variant, the first 128 bytes of each frame of its waves' tiles.  The rewrite patches the
+// staged rows, and only the 16-byte chunks it touched go back to HBM; payload bytes are never
+// read.  At most one hop field is checked per frame (ingress from a neighbour AS or
 // egress of a packet from the own AS), with the record-verify kernel's AES code (slot-0 key
 // in SGPRs).
 #include <hip/hip_runtime.h>
@@ -137,9 +137,9 @@ struct BrFrame {
 // Header reads (the BPF code's little-endian loads of network-order fields): bytes inside the
 // staged window come from LDS (a 32-bit field = two aligned ds_read_b32 + v_alignbyte), the
 // rest from the frame in HBM.  The LDS read is unconditional (clamped into the row) and only
-// the rare read past the window is a branch: with the LDS read inside the branch, every header
-// field cost its own basic block and a full LDS round trip (s_waitcnt lgkmcnt(0) per field), so
-// nothing overlapped the parse's ~300 LDS latencies.
+// the rare read past the window is a branch, so reads of independent fields can share one wait
+// (1 % faster than the LDS read inside the branch: most of the parse's waits are data-dependent,
+// each offset coming from the previous field).
 __device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
 {
     const uint32_t *row = s_hdr + k.row;

@@ -1690,6 +1690,8 @@ int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count,
                     float *kernel_ms)
 {
     if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
+    struct timespec t_in, t_chk, t_beg;
+    clock_gettime(CLOCK_MONOTONIC, &t_in);
     *first_ticket = 0;
     if (kernel_ms) *kernel_ms = 0.0f;
     for (size_t i = 0; i < count; ++i) {
@@ -1703,9 +1705,11 @@ int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count,
     DeviceGuard g(ctx->device);
     int rc = svc_quiesce(ctx);
     if (rc) return rc;
+    clock_gettime(CLOCK_MONOTONIC, &t_chk);
     DevState *ds;
     rc = svc_begin(ctx, ctx->svc_idle_ms, &ds);
     if (rc) return rc;
+    clock_gettime(CLOCK_MONOTONIC, &t_beg);
     // the batches, then the stop right behind them, are in the ring before the grid starts (a
     // longer run launches once the ring is full): the grid exits as soon as its blocks finish
     // their share of the last batch, with no stop to post and relay afterwards
@@ -1740,8 +1744,11 @@ int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count,
         auto us = [](const timespec &a, const timespec &b) {
             return (b.tv_sec - a.tv_sec) * 1e6 + (b.tv_nsec - a.tv_nsec) / 1e3;
         };
-        fprintf(stderr, "hfv_service_run: launch call %.1f us, launch return -> grid exit seen %.1f us, grid %.1f us\n",
-                us(t_post, t_launch), us(t_launch, t_done), kernel_ms ? *kernel_ms * 1e3 : -1.0);
+        fprintf(stderr,
+                "hfv_service_run: checks+guard+quiesce %.1f us, begin %.1f us, posts %.1f us, launch call %.1f us, "
+                "launch return -> grid exit seen %.1f us, grid %.1f us\n",
+                us(t_in, t_chk), us(t_chk, t_beg), us(t_beg, t_post), us(t_post, t_launch), us(t_launch, t_done),
+                kernel_ms ? *kernel_ms * 1e3 : -1.0);
     }
     return rc ? rc : sr;
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Headline run-to-run spread with the launching thread pinned to the GPU's NUMA node
 # (HFV_BENCH_PIN=1, default) or left where it starts (0).  scripts/bench_pin_probe.sh ROUNDS
+# (The HFV_BENCH_PIN knob was removed after this A/B: no difference; profiles/r02/svc_ab/.)
 set -u
 R=${1:-5}
 for r in $(seq 1 $R); do

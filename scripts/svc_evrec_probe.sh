@@ -1,6 +1,7 @@
 #!/bin/bash
 # Headline timed regions with the service grid's timing events attached to the launch
 # (hipExtLaunchKernel, default) or recorded around a plain launch (HFV_SVC_EVREC=1).
+# (The HFV_SVC_EVREC knob was removed after this A/B: no difference; profiles/r02/svc_ab/.)
 set -u
 R=${1:-4}
 for r in $(seq 1 $R); do

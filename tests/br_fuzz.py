@@ -175,3 +175,25 @@ def fuzz_batch(hops, br, v6, n, seed, slot=T.SLOT, payload_max=0):
         lens[i] = ln
         ifidx[i] = ifi
     return frames, lens, ifidx
+
+
+def with_ipv4_options(frame: bytes, k: int) -> bytes:
+    """The IPv4 frame with k NOP option words after its 20-byte header (IHL 5 + k): everything
+    from the UDP header on moves by 4k bytes.  The router does not check the IPv4 total length
+    or header checksum (it updates the checksum incrementally, parser.h:72-96), so the frame is
+    routed as before; its fields land 4k bytes further into the 128-byte staging window."""
+    g = bytearray(frame[:34])
+    g[14] = 0x40 | (5 + k)
+    return bytes(g) + bytes([1]) * (4 * k) + frame[34:]
+
+
+def options_shift_batch(hops, br="br1"):
+    """Every IPv4 hop input of `br`, with 0..10 option words: (frames, lens, ifindex, rows)."""
+    mine = [(i, f) for b, i, f in hops if b == br]
+    frames_l, ifis = [], []
+    for k in range(11):
+        for ifi, f in mine:
+            frames_l.append(with_ipv4_options(f, k))
+            ifis.append(ifi)
+    frames, lens = T.to_slots(frames_l)
+    return frames, lens, np.array(ifis, dtype=np.uint32), len(mine)

@@ -206,3 +206,15 @@ def test_segid_rewrite_inside_checked_hop_field(v6):
     a, v, e, _ = br.process(buf, lens, np.array([ifi], dtype=np.uint32))
     assert (a[0], v[0]) == (4, V["SCION_FORWARD"])
     assert buf[0, :len(want)].tobytes() == want
+
+
+def test_ipv4_options_move_fields_not_outcomes():
+    """IPv4 options shift the SCION header by 4..40 bytes (parser.h:60-66 skips IHL * 4 - 20):
+    every hop input of BR 1 gets the same action, verdict and egress with 0..10 option words
+    (the GPU test of the same batch puts fields on both sides of the kernel's 128-byte window)."""
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    frames, lens, ifidx, m = F.options_shift_batch(F.hop_inputs(brs, False, MAC))
+    a, v, e, _ = orc.br_process(frames, lens, ifidx, T.br_config("br1"), orc.hop_key(T.KEYS[1]))
+    a, v, e = (x.reshape(11, m) for x in (a, v, e))
+    assert (a == a[0]).all() and (v == v[0]).all() and (e == e[0]).all()
+    assert (v[0] == V["SCION_FORWARD"]).sum() >= m // 2

@@ -62,6 +62,16 @@ def test_segid_rewrite_inside_checked_hop_field(gpu_ctx, v6):
     assert got[0, :len(want)].tobytes() == want
 
 
+def test_ipv4_options_across_the_window(gpu_ctx):
+    """IPv4 options (IHL 6..15) move PathMeta, the info and hop fields and the rewritten SegIDs
+    4..40 bytes further, so the kernel's reads and writes fall inside, across and past its
+    128-byte staging window: bit-exact against the oracle, and routed like the unshifted frames."""
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    frames, lens, ifidx, m = F.options_shift_batch(F.hop_inputs(brs, False, MAC))
+    v = _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[1]).reshape(11, m)
+    assert (v == v[0]).all() and (v[0] == hfv.VERDICT["SCION_FORWARD"]).sum() >= m // 2
+
+
 @pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
 @pytest.mark.parametrize("br", ["br1", "br2", "br3"])
 def test_fuzz_parity(gpu_ctx, br, v6):

@@ -103,7 +103,6 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
         for (int w = 0; w < 4; ++w) {
             d.remote[w] = le32(a.remote + 4 * w);
             d.local[w] = le32(a.local + 4 * w);
-            d.remote_be[w] = be32(a.remote + 4 * w);
         }
         d.remote_port = le16(a.remote_port);
         d.local_port = le16(a.local_port);
@@ -150,7 +149,7 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out)
             const DevBrRoute &rt = out->routes[r];
             if (rt.family != e.family) continue;
             uint32_t diff = 0;
-            for (int w = 0; w < 4; ++w) diff |= (e.remote_be[w] ^ rt.pfx[w]) & rt.mask[w];
+            for (int w = 0; w < 4; ++w) diff |= (__builtin_bswap32(e.remote[w]) ^ rt.pfx[w]) & rt.mask[w];   // big-endian words
             if (diff == 0 && (best < 0 || rt.plen > best_len)) {
                 best = (int)r;
                 best_len = rt.plen;

@@ -43,7 +43,6 @@ struct DevBrIngress {        // ingress_map key {ipv4, ipv6[4], port, u16 ifinde
 struct DevBrEgress {
     uint32_t ifid, fwd_external, family;
     uint32_t remote[4], local[4];   // l32 words
-    uint32_t remote_be[4];          // big-endian words of remote (route lookup key)
     uint32_t remote_port, local_port;   // l16
     // resolved at compile time from the static tables (the per-frame lookups' results depend
     // only on the entry): the next-hop route of `remote` (-1: none) and, for a sibling, the

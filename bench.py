@@ -328,9 +328,14 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     svc = {}
     posts = ctx.service_batches([(batches[k % R], n, bitmaps[k % nb]) for k in range(steps)])
 
+    run_async = os.environ.get("HFV_BENCH_ASYNC", "0") != "0"
+
     def service_run():
         t = time.perf_counter()
-        svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
+        if run_async:   # the region's closing device synchronize waits for the grid
+            ctx.service_run_async(posts)
+        else:
+            svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
         svc["call_us"] = (time.perf_counter() - t) * 1e6
 
     # the K-step timed region is repeated `reps` times (each a fresh grid over the same K
@@ -342,6 +347,8 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
             b.zero_()
         W.sync()
         el, per_rank = W.timed(1, service_run)
+        if run_async:
+            svc["grid_ms"] = ctx.service_stop()   # reaps the exited grid: its lifetime
         runs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"]))   # diagnostics
         check(steps)
     runs.sort(key=lambda r: r[0])

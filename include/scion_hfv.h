@@ -197,6 +197,11 @@ int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t co
  * (nullable).  For a known set of batches it saves posting and relaying a stop afterwards. */
 int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
                     float *kernel_ms);
+/* The same without the wait: returns once the grid is launched with the batches and the stop
+ * behind them, so a caller that synchronizes the device (or the tickets) anyway does not wait
+ * twice.  The grid exits by itself after the last batch; hfv_service_stop (or any later data-path
+ * call) reaps it and reports its lifetime. */
+int hfv_service_run_async(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket);
 /* Tickets are monotonic over the ctx's life, across service restarts (key changes, idle
  * exits): a ticket of a stopped grid reports done, or -EIO if that grid exited on its idle
  * timeout without verifying it. */

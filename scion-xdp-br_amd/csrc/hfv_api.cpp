@@ -1685,8 +1685,22 @@ int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t co
     return launch ? svc_launch(ctx, launch) : 0;
 }
 
+static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
+                   float *kernel_ms, bool wait);
+
 int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
                     float *kernel_ms)
+{
+    return svc_run(ctx, batches, count, first_ticket, kernel_ms, true);
+}
+
+int hfv_service_run_async(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket)
+{
+    return svc_run(ctx, batches, count, first_ticket, nullptr, false);
+}
+
+static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket,
+                   float *kernel_ms, bool wait)
 {
     if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
     struct timespec t_in, t_chk, t_beg;
@@ -1736,6 +1750,7 @@ int hfv_service_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count,
         if (lr) return lr;
     }
     clock_gettime(CLOCK_MONOTONIC, &t_launch);
+    if (!wait) return rc;   // the grid exits after the stop posted behind the batches
     int sr = svc_stop(ctx, kernel_ms);
     clock_gettime(CLOCK_MONOTONIC, &t_done);
     static const bool trace = getenv("HFV_SVC_TRACE") != nullptr;   // diagnostics

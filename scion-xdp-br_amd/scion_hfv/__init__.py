@@ -100,6 +100,7 @@ def lib():
         "hfv_service_submit": (i32, [vp, vp, sz, sz, vp, ctypes.POINTER(u64)]),
         "hfv_service_submitv": (i32, [vp, vp, sz, ctypes.POINTER(u64)]),
         "hfv_service_run": (i32, [vp, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
+        "hfv_service_run_async": (i32, [vp, vp, sz, ctypes.POINTER(u64)]),
         "hfv_service_poll": (i32, [vp, u64]),
         "hfv_service_wait": (i32, [vp, u64, i32]),
         "hfv_service_stop": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
@@ -458,6 +459,15 @@ class Ctx:
         ms = ctypes.c_float(0.0)
         _check(lib().hfv_service_run(self._h, arr, len(arr), ctypes.byref(t), ctypes.byref(ms)))
         return list(range(t.value, t.value + len(arr))), ms.value
+
+    def service_run_async(self, batches):
+        """hfv_service_run without the wait: the grid is launched with the batches and the stop
+        behind them; a device synchronize (or service_wait) covers it, service_stop reaps it and
+        returns its lifetime.  Returns the tickets."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        t = ctypes.c_uint64()
+        _check(lib().hfv_service_run_async(self._h, arr, len(arr), ctypes.byref(t)))
+        return list(range(t.value, t.value + len(arr)))
 
     def service_poll(self, ticket):
         rc = lib().hfv_service_poll(self._h, ticket)

@@ -199,6 +199,29 @@ def test_service_submitv_golden_ifid(ctx):
         assert np.array_equal(bits_np(o, b - a), orc.verify_records(g["records"][a:b], hk, valid, 1))
 
 
+@pytest.mark.parametrize("count", [1, 20, 300], ids=["one", "twenty", "past_ring"])
+def test_service_run_async(ctx, count):
+    """hfv_service_run_async: returns once the grid is launched; a device synchronize covers
+    the whole run (the grid exits by itself behind its stop), bitmaps equal the oracle's, and
+    service_stop reaps the grid and reports its lifetime."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    torch.cuda.synchronize()
+    cuts = [(k * 11) % (n - 64) for k in range(count)]
+    outs = [new_bits(n - c, fill=-1) for c in cuts]
+    ts = ctx.service_run_async([(d[c:], n - c, o) for c, o in zip(cuts, outs)])
+    assert len(ts) == count
+    torch.cuda.synchronize()
+    for t in ts:
+        assert ctx.service_poll(t)
+    hk, valid = orc.key_table(orc.KEY_1111)
+    for c, o in zip(cuts, outs):
+        assert np.array_equal(bits_np(o, n - c), orc.verify_records(g["records"][c:], hk, valid, 0))
+    assert ctx.service_stop() > 0 and not ctx.service_running
+
+
 @pytest.mark.parametrize("count", [1, 5, 300], ids=["one", "five", "past_ring"])
 def test_service_run_one_shot(ctx, count):
     """hfv_service_run: batches + stop posted before the grid starts (a run longer than the

@@ -328,7 +328,10 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     svc = {}
     posts = ctx.service_batches([(batches[k % R], n, bitmaps[k % nb]) for k in range(steps)])
 
-    run_async = os.environ.get("HFV_BENCH_ASYNC", "0") != "0"
+    # hfv_service_run_async: the region's closing device synchronize is the only wait (the
+    # waiting hfv_service_run, HFV_BENCH_ASYNC=0, spins on the grid's stream first: ~5 % slower,
+    # profiles/r02/svc_ab/run_async_ab_r02f2.log)
+    run_async = os.environ.get("HFV_BENCH_ASYNC", "1") != "0"
 
     def service_run():
         t = time.perf_counter()
@@ -817,8 +820,9 @@ def run_hf(args, W):
                               f"per GPU > 256 MiB Infinity Cache): records are read from HBM"),
         "ceilings": ceilings(args.keysel, n, m["mhz"], cus),
         "path": ("resident service: one persistent grid; the K batches and a stop descriptor posted through the "
-                 "host descriptor ring by one hfv_service_run call, which launches the grid after them and waits for "
-                 "it; posting, grid launch, table fill and drain inside the timed region"
+                 "host descriptor ring by one hfv_service_run_async call, which launches the grid after them; the "
+                 "timed region's closing device synchronize waits for the grid to exit; posting, grid launch, table "
+                 "fill and drain inside the timed region"
                  if headline == "service" else "one hfv_verify_records launch per batch"),
         "service": None if args.launch_only else {
             "mpkts": round(total * args.steps / m["svc_el"] / 1e6, 2),

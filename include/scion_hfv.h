@@ -337,6 +337,14 @@ int hfv_br_load_config(hfv_ctx *ctx, const char *toml_path, const struct hfv_br_
 int hfv_brconfig_path(const char *br, char *out, size_t len);
 int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg);
 int hfv_brconfig_read(const char *path, struct hfv_br_config *cfg);
+/* `hfv-loader detach`: marks the pinned tables detached (the file stays, so data planes that
+ * attached it see the change): from their next batch an attached ctx passes every frame
+ * (action XDP_PASS, verdict 0, egress -1, nothing counted), as the interface does once
+ * detachBr removed the XDP program (br_loader.cpp:153-162); a later hfv_brconfig_publish
+ * re-attaches.  -ENOENT if the file is missing or already detached.  Publish and read reject
+ * tables whose counts exceed the fixed capacity (-EINVAL), and an attached ctx keeps its
+ * previous tables (and fails that call) when it finds such a snapshot. */
+int hfv_brconfig_detach(const char *path);
 int hfv_ctx_attach_brconfig(hfv_ctx *ctx, const char *path);
 /* Process n frames in place.  pkts: frame i at pkts + i*slot (slot % 8 == 0, >= 64);
  * len[i] its length (<= slot); ingress_ifindex[i] the receiving interface.  Outputs per

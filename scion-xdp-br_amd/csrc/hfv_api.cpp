@@ -183,6 +183,8 @@ struct hfv_ctx {
     // publication
     DevState *host_img = nullptr;         // pinned staging image
     hipEvent_t img_free = nullptr;        // staging image may be rewritten once this fires
+                                          // (= the last publish copy into dev_tab[active] is done)
+    bool pub_pending = false;             // img_free not yet seen complete: other streams wait on it
     DevState *dev_tab[2] = {nullptr, nullptr};
     hipStream_t readers[2][8] = {};                // streams that launched with dev_tab[i]
     hipEvent_t reader_ev[2][8] = {};               // caller streams: recorded after each such launch
@@ -264,7 +266,15 @@ static hipStream_t pick_stream(hfv_ctx *, void *stream) { return (hipStream_t)st
 static void note_reader(hfv_ctx *ctx, hipStream_t st);
 static bool own_stream(const hfv_ctx *ctx, hipStream_t st);
 
-// Make the shadow table visible to work enqueued next on `st`; returns the table to use.
+// HFV_PUB_FENCE=0 builds the round-2 behaviour (no cross-stream wait for a publish copy) for the
+// A/B that names the loop failure's cause (`make nofence`); never a product build.
+#ifndef HFV_PUB_FENCE
+#define HFV_PUB_FENCE 1
+#endif
+
+// Make the shadow table visible to work enqueued next on `st` -- and, once the copy is queued,
+// to work on any other stream (which waits for the copy until it has been seen complete);
+// returns the table to use.
 static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
 {
     if (ctx->keymap) {   // pick up updates other processes made to the pinned map
@@ -278,10 +288,15 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         uint32_t seq = brcfg_seq(ctx->brmap);
         if (seq != ctx->brmap_seq) {
             hfv_br_config cfg;
-            ctx->brmap_seq = brcfg_snapshot(ctx->brmap, &cfg);
+            uint32_t detached = 0;
+            ctx->brmap_seq = brcfg_snapshot(ctx->brmap, &cfg, &detached);
+            if (br_config_check(&cfg) != 0)   // a corrupt or foreign file: keep the tables in use
+                return fail(-EINVAL, "attached router config holds counts past the fixed capacity; "
+                                     "previous tables kept");
             const uint32_t off = ctx->br.hf_check_off;
             compile_br_config(&cfg, &ctx->br);
             ctx->br.hf_check_off = off;
+            ctx->br.detached = detached;
             ctx->dirty = true;
         }
     }
@@ -318,6 +333,15 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
         ctx->dirty = false;
+        ctx->pub_pending = true;
+    } else if (HFV_PUB_FENCE && ctx->pub_pending) {
+        // The copy into dev_tab[active] was enqueued on the stream that published it; work on any
+        // other stream must not read the table before that copy lands.  (Round 2 skipped this: the
+        // config-5 loop published on its chunk-0 stream and launched chunk 1 on a second stream,
+        // whose kernel could read the half-written or previous table -- every MAC of that chunk
+        // failed against a stale key, gpurun_out/r02c5: tx short by exactly one chunk.)
+        if (hipEventQuery(ctx->img_free) == hipSuccess) ctx->pub_pending = false;
+        else HIP_TRY(hipStreamWaitEvent(st, ctx->img_free, 0));
     }
     *out = ctx->dev_tab[ctx->active];
     return 0;
@@ -760,8 +784,7 @@ int hfv_verdict_counters(hfv_ctx *ctx, const void *recs, size_t stride, size_t n
 int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
 {
     if (!ctx || !cfg) return fail(-EINVAL, "null argument");
-    if (cfg->n_int_ifaces > HFV_BR_MAX_IFACES || cfg->n_ingress > HFV_BR_MAX_IFACES ||
-        cfg->n_egress > HFV_BR_MAX_IFACES || cfg->n_routes > HFV_BR_MAX_ROUTES || cfg->n_tx_ports > HFV_BR_MAX_TXPORTS)
+    if (br_config_check(cfg))
         return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
                     HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
     const uint32_t off = ctx->br.hf_check_off;
@@ -1192,8 +1215,14 @@ void hfv::forget_stream(hfv_ctx *ctx, void *stream)
 {
     for (int a = 0; a < 2; ++a)
         for (int r = 0; r < ctx->nreaders[a];)
-            if (ctx->readers[a][r] == (hipStream_t)stream) ctx->readers[a][r] = ctx->readers[a][--ctx->nreaders[a]];
-            else ++r;
+            if (ctx->readers[a][r] == (hipStream_t)stream) {
+                // the last entry moves into slot r together with its fence event
+                const int last = --ctx->nreaders[a];
+                ctx->readers[a][r] = ctx->readers[a][last];
+                std::swap(ctx->reader_ev[a][r], ctx->reader_ev[a][last]);
+            } else {
+                ++r;
+            }
 }
 
 int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen,
@@ -1599,8 +1628,12 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
 int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
-    if (ctx->svc_running) return 0;
     DeviceGuard g(ctx->device);
+    if (ctx->svc_running && ctx->svc_stop_posted) {   // a run_async grid leaving on its own stop
+        int rc = svc_stop(ctx, nullptr);
+        if (rc) return rc;
+    }
+    if (ctx->svc_running) return 0;
     DevState *ds;
     int rc = svc_begin(ctx, idle_ms, &ds);
     if (rc) return rc;
@@ -1624,6 +1657,12 @@ static int svc_check_batch(const hfv_ctx *ctx, const void *recs, size_t stride, 
 static int svc_ready(hfv_ctx *ctx, DevState **launch)
 {
     *launch = nullptr;
+    if (ctx->svc_running && ctx->svc_stop_posted) {
+        // a grid started by hfv_service_run_async has its stop behind its batches and exits by
+        // itself: nothing posted now would be read, so reap it and begin a fresh grid
+        int rc = svc_stop(ctx, nullptr);
+        if (rc) return rc;
+    }
     if (ctx->svc_running && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0) {
         // the grid left on its idle timeout: reap it (batches it left unverified are recorded
         // as lost for hfv_service_wait/poll) and start a fresh one

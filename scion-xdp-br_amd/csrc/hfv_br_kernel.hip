@@ -762,6 +762,17 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     // launch of fewer tiles than waves (the config-5 loop's 64 Ki-frame chunks: 1024 tiles)
     // still spreads over every CU instead of filling a quarter of them with 16 waves each.
     uint64_t t = (uint64_t)wib * gridDim.x + blockIdx.x;
+    if (s_br.detached) {   // `hfv-loader detach`: no router on the interface, every frame goes up the stack
+        for (; t < ntiles; t += nwaves) {
+            const uint64_t i = t * 64 + lane;
+            if (i < n) {
+                action[i] = A_PASS;
+                verdict[i] = 0;
+                egress[i] = -1;
+            }
+        }
+        return;   // block-uniform: no barrier below is reached by only part of the block
+    }
     const uint32_t fr_of = lane / C, ch = lane % C;   // staging: frame within round, chunk
     // The tile's header rows and the lane's own length / ingress ifindex are loaded at the top
     // of each tile, with no register prefetch of the next tile: the other waves of the CU (16
@@ -870,6 +881,16 @@ extern "C" int hfv_debug_br_prof(unsigned long long out[8])
 }
 #endif
 
+// Test-only launch-geometry override (hfv_debug_br_grid): blocks per k_br_process launch, 0 =
+// one block per CU up to the tile count.  With 1, a 1000-frame chunk runs as 16 active waves of
+// one block -- the shape the round-2 loop failure ran in ("loop parity failure").
+static unsigned g_br_grid_override = 0;
+extern "C" int hfv_debug_br_grid(unsigned blocks)
+{
+    g_br_grid_override = blocks;
+    return 0;
+}
+
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
@@ -900,6 +921,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     }
     const uint64_t tiles = (n + 63) / 64, cap = (uint64_t)g.num_cus;   // one block per CU at most
     unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
+    if (g_br_grid_override && g_br_grid_override < grid) grid = g_br_grid_override;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,

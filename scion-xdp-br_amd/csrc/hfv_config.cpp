@@ -782,9 +782,11 @@ struct BrcfgFile {
     char magic[8];
     uint32_t version;
     uint32_t seq;          // seqlock: odd while a writer updates the tables
-    uint8_t reserved[48];
+    uint32_t detached;     // 1: `hfv-loader detach` -- attached data planes pass every frame
+    uint8_t reserved[44];
     hfv_br_config cfg;
 };
+static_assert(sizeof(BrcfgFile) == 64 + sizeof(hfv_br_config), "pinned file layout unchanged");
 static const char kBrMagic[8] = {'H', 'F', 'V', 'B', 'R', 'C', 'F', '1'};
 
 static int mkdir_parents(const char *path)
@@ -803,17 +805,33 @@ static int mkdir_parents(const char *path)
 
 }  // namespace
 
-// Consistent snapshot of a pinned br_config mapping; returns its (even) seq.
-uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out)
+// Consistent snapshot of a pinned br_config mapping (tables and detached flag); returns its
+// (even) seq.
+uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached)
 {
     const BrcfgFile *f = (const BrcfgFile *)mapping;
     for (;;) {
         uint32_t s0 = __atomic_load_n(&f->seq, __ATOMIC_ACQUIRE);
         if (s0 & 1u) { usleep(10); continue; }
         memcpy(out, &f->cfg, sizeof *out);
+        const uint32_t d = __atomic_load_n(&f->detached, __ATOMIC_RELAXED);
         std::atomic_thread_fence(std::memory_order_acquire);
-        if (__atomic_load_n(&f->seq, __ATOMIC_ACQUIRE) == s0) return s0;
+        if (__atomic_load_n(&f->seq, __ATOMIC_ACQUIRE) == s0) {
+            if (detached) *detached = d;
+            return s0;
+        }
     }
+}
+
+// Table counts within the fixed capacity of struct hfv_br_config / DevBrConfig: the compile
+// loops index the arrays by them, so a snapshot of a stale, foreign or corrupt pinned file is
+// checked before it is used.
+int br_config_check(const hfv_br_config *cfg)
+{
+    if (cfg->n_int_ifaces > HFV_BR_MAX_IFACES || cfg->n_ingress > HFV_BR_MAX_IFACES ||
+        cfg->n_egress > HFV_BR_MAX_IFACES || cfg->n_routes > HFV_BR_MAX_ROUTES || cfg->n_tx_ports > HFV_BR_MAX_TXPORTS)
+        return -EINVAL;
+    return 0;
 }
 uint32_t brcfg_seq(const void *mapping) { return __atomic_load_n(&((const BrcfgFile *)mapping)->seq, __ATOMIC_ACQUIRE); }
 
@@ -889,6 +907,9 @@ int hfv_brconfig_path(const char *br, char *out, size_t len)
 int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg)
 {
     if (!path || !cfg) return fail(-EINVAL, "null argument");
+    if (br_config_check(cfg))
+        return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
+                    HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
     int rc = mkdir_parents(path);
     if (rc) return fail(rc, "cannot create the directory of %s", path);
     int fd = open(path, O_RDWR | O_CREAT, 0644);
@@ -915,11 +936,45 @@ int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg)
     __atomic_store_n(&f->seq, f->seq + 1, __ATOMIC_RELAXED);   // odd: update in progress
     std::atomic_thread_fence(std::memory_order_release);
     f->cfg = *cfg;
+    __atomic_store_n(&f->detached, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(&f->seq, f->seq + 1, __ATOMIC_RELEASE);   // even: published
     msync(m, sizeof(BrcfgFile), MS_SYNC);
     munmap(m, sizeof(BrcfgFile));
     close(fd);
     return 0;
+}
+
+int hfv_brconfig_detach(const char *path)
+{
+    if (!path) return fail(-EINVAL, "null argument");
+    int fd = open(path, O_RDWR);
+    if (fd < 0) return fail(-ENOENT, "not attached: %s", path);
+    if (flock(fd, LOCK_EX) != 0) { int e = -errno; close(fd); return fail(e, "flock %s", path); }
+    struct stat st;
+    void *m = MAP_FAILED;
+    if (fstat(fd, &st) == 0 && (size_t)st.st_size == sizeof(BrcfgFile))
+        m = mmap(nullptr, sizeof(BrcfgFile), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED || memcmp(((BrcfgFile *)m)->magic, kBrMagic, 8) != 0) {
+        if (m != MAP_FAILED) munmap(m, sizeof(BrcfgFile));
+        close(fd);
+        return fail(-EINVAL, "%s is not a pinned router config", path);
+    }
+    BrcfgFile *f = (BrcfgFile *)m;
+    int rc = 0;
+    if (__atomic_load_n(&f->detached, __ATOMIC_RELAXED)) {
+        rc = fail(-ENOENT, "not attached: %s", path);
+    } else {
+        // the file stays (attached data planes keep their mapping of this inode and see the
+        // flag at their next batch; a later attach republishes into the same file)
+        __atomic_store_n(&f->seq, f->seq + 1, __ATOMIC_RELAXED);
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&f->detached, 1u, __ATOMIC_RELAXED);
+        __atomic_store_n(&f->seq, f->seq + 1, __ATOMIC_RELEASE);
+        msync(m, sizeof(BrcfgFile), MS_SYNC);
+    }
+    munmap(m, sizeof(BrcfgFile));
+    close(fd);
+    return rc;
 }
 
 int hfv_brconfig_read(const char *path, struct hfv_br_config *cfg)
@@ -928,8 +983,11 @@ int hfv_brconfig_read(const char *path, struct hfv_br_config *cfg)
     const void *m = nullptr;
     int rc = brcfg_open_ro(path, &m);
     if (rc) return fail(rc, "cannot open pinned router config %s", path);
-    brcfg_snapshot(m, cfg);
+    uint32_t detached = 0;
+    brcfg_snapshot(m, cfg, &detached);
     brcfg_close(m);
+    if (br_config_check(cfg)) return fail(-EINVAL, "pinned router config %s holds counts past the fixed capacity", path);
+    if (detached) return fail(-ENOENT, "not attached: %s (detached)", path);
     return 0;
 }
 

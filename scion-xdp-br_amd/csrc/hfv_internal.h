@@ -59,7 +59,9 @@ struct DevBrRoute {
 };
 struct DevBrConfig {
     uint32_t n_int, n_ing, n_egr, n_routes;
-    uint32_t hf_check_off, pad_[3];   // 1: the ENABLE_HF_CHECK=OFF router (hfv_br_set_hf_check)
+    uint32_t hf_check_off;   // 1: the ENABLE_HF_CHECK=OFF router (hfv_br_set_hf_check)
+    uint32_t detached;       // 1: the attached pinned config was detached -- every frame passes
+    uint32_t pad_[2];
     uint32_t tx_bits[HFV_BR_MAX_TXPORTS / 32];
     DevBrIntIface int_ifaces[HFV_BR_MAX_IFACES];
     DevBrIngress ingress[HFV_BR_MAX_IFACES];
@@ -178,7 +180,8 @@ int keymap_create(const char *path);   // empty map (header only) if the file do
 int brcfg_open_ro(const char *path, const void **mapping);
 void brcfg_close(const void *mapping);
 uint32_t brcfg_seq(const void *mapping);
-uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out);
+uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached);
+int br_config_check(const hfv_br_config *cfg);
 void keymap_close(const void *mapping);
 uint32_t keymap_seq(const void *mapping);
 uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8]);

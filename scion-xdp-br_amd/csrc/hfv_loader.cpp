@@ -314,7 +314,7 @@ static int detach(int argc, char **argv)
         fprintf(stderr, "Invalid border router name: %s\n", hfv_last_error());
         return EXIT_FAILURE;
     }
-    if (unlink(cpath) != 0) {
+    if (hfv_brconfig_detach(cpath) != 0) {   // the file stays: attached data planes see the flag
         fprintf(stderr, "Not attached: %s\n", cpath);
         return EXIT_FAILURE;
     }

@@ -84,6 +84,7 @@ def lib():
         "hfv_brconfig_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
         "hfv_brconfig_publish": (i32, [ctypes.c_char_p, vp]),
         "hfv_brconfig_read": (i32, [ctypes.c_char_p, vp]),
+        "hfv_brconfig_detach": (i32, [ctypes.c_char_p]),
         "hfv_ctx_attach_brconfig": (i32, [vp, ctypes.c_char_p]),
         "hfv_br_process": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]),
         "hfv_br_process_timed": (i32, [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
@@ -394,6 +395,11 @@ class Ctx:
                 "gpu_busy_s": st.gpu_busy_s, "gpu_wait_s": st.gpu_wait_s, "producer_busy_s": st.producer_busy_s,
                 "consumer_busy_s": st.consumer_busy_s}
 
+    @staticmethod
+    def debug_br_grid(blocks):
+        """Test-only: cap k_br_process launches at `blocks` blocks (0 = default geometry)."""
+        _check(lib().hfv_debug_br_grid(ctypes.c_uint(blocks)))
+
     def host_register(self, buf):
         _check(lib().hfv_host_register(self._h, _ptr(buf), buf.nbytes))
 
@@ -667,6 +673,11 @@ def brconfig_read(path: str):
     cfg = BrConfig()
     _check(lib().hfv_brconfig_read(path.encode(), ctypes.byref(cfg)))
     return cfg
+
+
+def brconfig_detach(path: str):
+    """`hfv-loader detach`: attached data planes pass every frame from their next batch."""
+    _check(lib().hfv_brconfig_detach(path.encode()))
 
 
 # enum verdict (br/src/bpf/common.h:55-70)

@@ -91,8 +91,8 @@ def test_statsmap_and_watch(pin_dir):
 def test_cli_attach_detach(pin_dir, tmp_path):
     """`hfv-loader attach <config> [--route ...]` (attachBr, br_loader.cpp:88-151): prints the
     configuration listing, publishes the router tables under $HFV_PIN_DIR/<self>/br_config,
-    creates the pinned key and counter maps (reused on a second attach); `detach <br>` removes
-    the tables.  The tables are the ones hfv_br_config_load builds (checked against the Python
+    creates the pinned key and counter maps (reused on a second attach); `detach <br>` marks
+    the tables detached in place.  The tables are the ones hfv_br_config_load builds (checked against the Python
     loader in test_br_config.py)."""
     if not os.path.exists(LOADER):
         pytest.skip("hfv-loader not built")
@@ -127,5 +127,34 @@ def test_cli_attach_detach(pin_dir, tmp_path):
     bad = run("attach", str(tmp_path / "missing.toml"), env=env)
     assert bad.returncode != 0 and "Parsing configuration failed" in bad.stderr
     assert run("detach", "br1-x", env=env).returncode == 0
-    assert not os.path.exists(cpath)
-    assert run("detach", "br1-x", env=env).returncode != 0
+    # the file stays (an attached data plane keeps its mapping of this inode) and
+    # carries the detached state; reading it reports "not attached"
+    assert os.path.exists(cpath)
+    with pytest.raises(hfv.HfvError):
+        hfv.brconfig_read(cpath)
+    bad = run("detach", "br1-x", env=env)
+    assert bad.returncode != 0 and "Not attached" in bad.stderr
+    r = run("attach", str(conf), env=env)                             # re-attach: same file, attached again
+    assert r.returncode == 0, r.stderr
+    assert hfv.brconfig_read(cpath).n_egress == 2
+    assert run("detach", "no-such-br", env=env).returncode != 0
+
+
+def test_brconfig_rejects_tables_past_capacity(pin_dir):
+    """publish and read check the table counts against the fixed capacity, so a
+    corrupt or foreign pinned file cannot drive the compile loops past the arrays."""
+    import struct
+    path = hfv.brconfig_path("br-cap")
+    cfg = hfv.BrConfig()
+    cfg.n_routes = hfv.BR_MAX_ROUTES + 1
+    with pytest.raises(hfv.HfvError):
+        hfv.brconfig_publish(path, cfg)
+    cfg.n_routes = 1
+    hfv.brconfig_publish(path, cfg)
+    assert hfv.brconfig_read(path).n_routes == 1
+    # corrupt the pinned file's n_egress (third u32 of the tables, which start at byte 64)
+    with open(path, "r+b") as f:
+        f.seek(64 + 8)
+        f.write(struct.pack("<I", 1000))
+    with pytest.raises(hfv.HfvError):
+        hfv.brconfig_read(path)

@@ -278,3 +278,16 @@ def test_attached_pinned_brconfig_reloads(gpu_ctx, tmp_path, monkeypatch):
         ga, gv, ge = Pinned(gpu_ctx, None).process(got, lens, ifidx)
         assert (ga == oa).all() and (gv == ov).all() and (ge == oe).all() and (got == ref).all(), cfg_name
     assert ctypes.sizeof(hfv.BrConfig) > 0
+    # `hfv-loader detach`: the attached data plane sees the detached state at its
+    # next batch and passes every frame untouched, as an interface without the XDP program does
+    hfv.brconfig_detach(path)
+    got = frames.copy()
+    ga, gv, ge = Pinned(gpu_ctx, None).process(got, lens, ifidx)
+    assert (ga == 2).all() and (gv == 0).all() and (ge == -1).all() and (got == frames).all()
+    # a later attach republishes into the same file: the data plane routes again
+    hfv.brconfig_publish(path, T.br_config("br1"))
+    ref = frames.copy()
+    oa, ov, oe, _ = orc.br_process(ref, lens, ifidx, T.br_config("br1"), orc.hop_key(T.KEYS[1]))
+    got = frames.copy()
+    ga, gv, ge = Pinned(gpu_ctx, None).process(got, lens, ifidx)
+    assert (ga == oa).all() and (gv == ov).all() and (ge == oe).all() and (got == ref).all()

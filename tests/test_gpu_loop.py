@@ -60,6 +60,39 @@ def test_loop_matches_oracle(gpu_ctx, hf_check, dma):
     assert int(stats[E.RX_IFINDEX, 0].sum()) == total * E.FRAME_LEN
 
 
+@pytest.mark.parametrize("dma", [0, 2], ids=["zero_copy", "dma_in_zc_out"])
+def test_loop_single_block_chunks(gpu_ctx, dma):
+    """The round-2 failing shape, forced: each 1000-frame chunk runs as ONE 1024-thread block
+    whose 16 waves are all active (hfv_debug_br_grid(1)), zero-copy on the mapped ring, fresh
+    router tables and key published by the loop's first chunk (the loop's other streams must
+    wait for that publish).  Repeated so chunk 1 races the publish more than once."""
+    frames = _frame_mix(97, bad_every=5)
+    stats = np.zeros((hfv.BR_STATS_IFINDEX, 2, hfv.BR_COUNTERS), dtype=np.uint64)
+    want = _oracle(frames, 10007, True)
+    import torch
+    recs = torch.zeros((64, 64), dtype=torch.uint8, device="cuda:0")
+    bits = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    hfv.Ctx.debug_br_grid(1)
+    try:
+        for rep in range(3):
+            # both device tables get a wrong slot-0 key first (one publish each), so a launch
+            # reading a stale table fails every MAC
+            for wrong in (bytes(16), bytes(range(16))):
+                gpu_ctx.key_add(0, wrong)
+                gpu_ctx.verify_records(recs, 64, bits)
+                torch.cuda.synchronize()
+            E.setup_ctx(gpu_ctx, hf_check=True)
+            stats[:] = 0
+            got = gpu_ctx.loop_run(frames, np.full(97, E.FRAME_LEN), 10007, rx_ifindex=E.RX_IFINDEX, slot=SLOT,
+                                   chunk=1000, chunks=3, producers=2, consumers=3, digest=True, stats=stats,
+                                   dma=dma)
+            for k in want:
+                assert got[k] == want[k], (rep, k)
+            assert [int(x) for x in stats[E.RX_IFINDEX, 1]] == want["verdicts"]
+    finally:
+        hfv.Ctx.debug_br_grid(0)
+
+
 def test_loop_more_threads_than_ring_chunks(gpu_ctx):
     """Producers and consumers outnumber the ring's chunks (chunks k and k + chunks share a slot
     and belong to different threads), three chunks in flight on the GPU."""

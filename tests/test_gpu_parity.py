@@ -153,6 +153,35 @@ def test_key_update_is_stream_ordered(ctx):
     assert np.array_equal(bits_np(outs[2], n), g["pass_bits"])
 
 
+def test_key_publish_visible_on_other_streams(ctx):
+    """A table published by a launch on stream A, its copy queued behind earlier work on A, is
+    the table a launch on stream B then reads: B waits for A's publish copy.  Round 2 had no
+    such fence; the config-5 loop published on its chunk-0 stream and its chunk-1 kernel, on a
+    second stream, could read the previous table (loop parity failure)."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    scratch = new_bits(n)
+    # two publishes of wrong keys: both device tables hold a key that fails these records
+    for wrong in (bytes(16), bytes(range(16))):
+        ctx.key_add(0, wrong)
+        ctx.verify_records(d, n, scratch, stream=a)
+        torch.cuda.synchronize()
+        assert not bits_np(scratch, n).any() or not np.array_equal(bits_np(scratch, n), g["pass_bits"])
+    ctx.key_add(0, orc.KEY_1111)
+    outs = [new_bits(n) for _ in range(3)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(a):
+        torch.cuda._sleep(20_000_000)   # stream A busy for milliseconds before the publish copy
+    ctx.verify_records(d, n, outs[0], stream=a)    # publishes: copy queued on A behind the sleep
+    ctx.verify_records(d, n, outs[1], stream=b)    # must not run before that copy lands
+    ctx.verify_records(d, n, outs[2], stream=0)    # nor on HIP's default stream
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(bits_np(o, n), g["pass_bits"])
+
+
 def test_partial_key_table_ifid(ctx):
     g = orc.load_golden("hf_ifid256.npz")
     n = len(g["records"])

@@ -222,6 +222,36 @@ def test_service_run_async(ctx, count):
     assert ctx.service_stop() > 0 and not ctx.service_running
 
 
+@pytest.mark.parametrize("then", ["submit", "submitv", "start_submit"])
+def test_service_submit_after_run_async(ctx, then):
+    """after hfv_service_run_async the grid exits on its own stop; a later
+    submit (or start + submit) with no service_stop in between must reap it and post to a
+    fresh grid, so the new tickets complete instead of sitting in a ring nobody reads."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    first = [new_bits(n, fill=-1) for _ in range(3)]
+    torch.cuda.synchronize()
+    ts = ctx.service_run_async([(d, n, o) for o in first])
+    outs = [new_bits(n, fill=-1) for _ in range(2)]
+    torch.cuda.synchronize()
+    if then == "submit":
+        new = [ctx.service_submit(d, n, o) for o in outs]
+    elif then == "submitv":
+        new = ctx.service_submitv([(d, n, o) for o in outs])
+    else:
+        ctx.service_start()
+        assert ctx.service_running
+        new = [ctx.service_submit(d, n, o) for o in outs]
+    assert new[0] > ts[-1]
+    for t in ts + list(new):
+        ctx.service_wait(t, 20000)
+        assert ctx.service_poll(t) == 1
+    for o in first + outs:
+        assert np.array_equal(bits_np(o, n), g["pass_bits"])
+
+
 @pytest.mark.parametrize("count", [1, 5, 300], ids=["one", "five", "past_ring"])
 def test_service_run_one_shot(ctx, count):
     """hfv_service_run: batches + stop posted before the grid starts (a run longer than the

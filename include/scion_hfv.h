@@ -107,12 +107,27 @@ int hfv_key_get(hfv_ctx *ctx, uint32_t index, struct hop_key *out);
  * 191, 221-222).  Path: $HFV_PIN_DIR/<br>/mac_key_map, HFV_PIN_DIR defaults to /dev/shm/hfv.
  * Writers serialise with flock; readers see whole updates (seqlock). */
 int hfv_keymap_path(const char *br, char *out, size_t len);
-/* Map::update of one slot, creating the map file if needed. */
+/* Map modes, fixed when the map is created:
+ *   HFV_KEYMAP_SLOTS  256 direct slots, index 0..255 (per-interface keys, config 3);
+ *   HFV_KEYMAP_HASH8  the reference map's semantics (maps.h:60-67: BPF_MAP_TYPE_HASH, u32
+ *                     index, max_entries 8): any u32 index, a 9th new index fails with -E2BIG
+ *                     as bpf_map_update_elem does.  The data plane reads indices < 256 (slot 0
+ *                     in the reference's single-key mode, xdp.c:82); larger ones are kept and
+ *                     listed but never looked up.  `hfv-loader` creates this mode. */
+#define HFV_KEYMAP_SLOTS 0
+#define HFV_KEYMAP_HASH8 1
+/* Map::update (BPF_ANY) of one index, creating a SLOTS map file if needed. */
 int hfv_keymap_update(const char *path, uint32_t index, const struct hop_key *hk);
 /* An empty map (no slot written) if the file does not exist yet; an existing map is kept. */
 int hfv_keymap_create(const char *path);
-/* Map::erase of one slot; -ENOENT if it was empty. */
+/* The same with the mode; an existing map without keys takes the mode, one with keys keeps its own. */
+int hfv_keymap_create_mode(const char *path, int mode);
+/* The map's mode (>= 0) or a negative errno. */
+int hfv_keymap_mode(const char *path);
+/* Map::erase of one index; -ENOENT if it was empty. */
 int hfv_keymap_erase(const char *path, uint32_t index);
+/* Every entry (index ascending) into indices[]/keys[] up to cap; *count = number of entries. */
+int hfv_keymap_list(const char *path, uint32_t *indices, struct hop_key *keys, size_t cap, size_t *count);
 /* Consistent snapshot of all HFV_MAX_KEYS slots and the 256-bit valid mask. */
 int hfv_keymap_read(const char *path, struct hop_key *slots, uint32_t *valid);
 /* reusePinnedMap: the ctx reloads its key table from the pinned map whenever the map

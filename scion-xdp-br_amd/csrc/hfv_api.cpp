@@ -272,6 +272,15 @@ static bool own_stream(const hfv_ctx *ctx, hipStream_t st);
 #define HFV_PUB_FENCE 1
 #endif
 
+// Test-only (hfv_debug_publish_delay): every publish copy waits behind a spin of this many
+// microseconds on its stream, so a test can make the cross-stream race deterministic.
+static uint32_t g_pub_delay_us = 0;
+extern "C" int hfv_debug_publish_delay(uint32_t us)
+{
+    g_pub_delay_us = us;
+    return 0;
+}
+
 // Make the shadow table visible to work enqueued next on `st` -- and, once the copy is queued,
 // to work on any other stream (which waits for the copy until it has been seen complete);
 // returns the table to use.
@@ -329,6 +338,7 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         }
         ctx->nreaders[next] = 0;
         ctx->readers_overflow[next] = false;
+        if (g_pub_delay_us) HIP_TRY((hipError_t)launch_debug_spin(st, g_pub_delay_us));
         HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
@@ -555,7 +565,7 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path)
     const void *m = nullptr;
     int rc = keymap_open_ro(path, &m);
     if (rc == -ENOENT) {   // create an empty pinned map, as attachBr creates mac_key_map
-        rc = keymap_create(path);   // header only: never touches a slot another process may write
+        rc = keymap_create(path, HFV_KEYMAP_SLOTS);   // header only: never touches a slot another process may write
         if (!rc) rc = keymap_open_ro(path, &m);
     }
     if (rc) return fail(rc, "cannot attach key map %s", path);

@@ -168,6 +168,8 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).
+// Diagnostics: one wave spinning for `us` microseconds (s_memrealtime) on `stream`.
+int launch_debug_spin(void *stream, uint32_t us);
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
@@ -175,7 +177,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
 
 // pinned key map (hfv_keymap.cpp)
 int keymap_open_ro(const char *path, const void **mapping);
-int keymap_create(const char *path);   // empty map (header only) if the file does not exist
+int keymap_create(const char *path, uint32_t mode);   // empty map (header only) if the file does not exist
 // pinned router tables (hfv_config.cpp)
 int brcfg_open_ro(const char *path, const void **mapping);
 void brcfg_close(const void *mapping);

@@ -1,7 +1,10 @@
 // hfv-loader -- control-plane CLI for the MI355X hop-field verifier, the counterpart of the
 // reference's `br-loader key add|remove` (br/src/br_loader.cpp:50-61, 182-295).
 //
-//   hfv-loader key add <br> <index> <base64-key>    decode, expand, derive K1, update map
+//   hfv-loader key add <br> <index> <base64-key>    decode, expand, derive K1, update map (any u32
+//                                                   index, at most 8 keys: the reference map's
+//                                                   semantics, maps.h:60-67; 0..255 and 256 keys
+//                                                   in a map `attach --key-slots` created)
 //   hfv-loader key remove <br> <index>              erase the slot (it then fails closed)
 //   hfv-loader key list <br>                        print occupied slots and K1 of each
 //   hfv-loader watch <br> <iface> [seconds]         verdict counters of one ingress port,
@@ -40,7 +43,7 @@ static void print_usage()
             "                  key remove <br> <index>\n"
             "                  key list <br>\n"
             "       hfv-loader watch <br> <iface> [seconds]\n"
-            "       hfv-loader attach <config> [--route <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]]...\n"
+            "       hfv-loader attach <config> [--key-slots] [--route <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]]...\n"
             "                  detach <br>\n");
 }
 
@@ -87,7 +90,9 @@ static int add_key(int argc, char **argv)
     struct aes_block subkeys[2];
     aes_cmac_subkeys(&hk.key, subkeys);
     hk.subkey = subkeys[0];
-    if (hfv_keymap_update(path, index, &hk) != 0) {
+    // a map this command has to create gets the reference map's semantics (u32 index, at most
+    // 8 entries, maps.h:60-67); one `attach --key-slots` created keeps its 256 direct slots
+    if (hfv_keymap_create_mode(path, HFV_KEYMAP_HASH8) != 0 || hfv_keymap_update(path, index, &hk) != 0) {
         fprintf(stderr, "Update failed: %s\n", hfv_last_error());
         return EXIT_FAILURE;
     }
@@ -116,16 +121,16 @@ static int list_keys(int argc, char **argv)
     if (argc < 1) { print_usage(); return EXIT_FAILURE; }
     char path[4096];
     if (map_path(argv[0], path, sizeof path)) return EXIT_FAILURE;
-    static struct hop_key slots[HFV_MAX_KEYS];
-    uint32_t valid[8];
-    if (hfv_keymap_read(path, slots, valid) != 0) {
+    static uint32_t idx[HFV_MAX_KEYS + 8];
+    static struct hop_key keys[HFV_MAX_KEYS + 8];
+    size_t n = 0;
+    if (hfv_keymap_list(path, idx, keys, HFV_MAX_KEYS + 8, &n) != 0) {
         fprintf(stderr, "Cannot read key map: %s\n", hfv_last_error());
         return EXIT_FAILURE;
     }
-    for (uint32_t k = 0; k < HFV_MAX_KEYS; ++k) {
-        if (!((valid[k >> 5] >> (k & 31)) & 1u)) continue;
-        printf("%u K1=", k);
-        for (int i = 0; i < 16; ++i) printf("%02x", slots[k].subkey.b[i]);
+    for (size_t k = 0; k < n && k < HFV_MAX_KEYS + 8; ++k) {
+        printf("%u K1=", idx[k]);
+        for (int i = 0; i < 16; ++i) printf("%02x", keys[k].subkey.b[i]);
         printf("\n");
     }
     return EXIT_SUCCESS;
@@ -261,10 +266,15 @@ static int attach(int argc, char **argv)
     if (argc < 1) { print_usage(); return EXIT_FAILURE; }
     static struct hfv_br_next_hop hops[HFV_BR_MAX_ROUTES];
     size_t nh = 0;
+    int kmode = HFV_KEYMAP_HASH8;   // the reference's mac_key_map (maps.h:60-67)
     for (int i = 1; i < argc; ++i) {
         if (strcmp(argv[i], "--route") == 0 && i + 1 < argc && nh < HFV_BR_MAX_ROUTES && parse_route(argv[i + 1], &hops[nh])) {
             ++nh;
             ++i;
+            continue;
+        }
+        if (strcmp(argv[i], "--key-slots") == 0) {   // 256 direct slots (per-interface keys)
+            kmode = HFV_KEYMAP_SLOTS;
             continue;
         }
         fprintf(stderr, "Invalid argument: %s\n", argv[i]);
@@ -286,7 +296,7 @@ static int attach(int argc, char **argv)
     }
     // reusePinnedMap: keys and counters survive a re-attach (br_loader.cpp:119-126)
     if (access(kpath, F_OK) == 0) printf("Reusing pinned map: \"%s\"\n", kpath);
-    else if (hfv_keymap_create(kpath) != 0) {
+    else if (hfv_keymap_create_mode(kpath, kmode) != 0) {
         fprintf(stderr, "Cannot create key map: %s\n", hfv_last_error());
         return EXIT_FAILURE;
     }

@@ -74,6 +74,9 @@ def lib():
         "hfv_keymap_update": (i32, [ctypes.c_char_p, u32, vp]),
         "hfv_keymap_erase": (i32, [ctypes.c_char_p, u32]),
         "hfv_keymap_read": (i32, [ctypes.c_char_p, vp, vp]),
+        "hfv_keymap_create_mode": (i32, [ctypes.c_char_p, i32]),
+        "hfv_keymap_mode": (i32, [ctypes.c_char_p]),
+        "hfv_keymap_list": (i32, [ctypes.c_char_p, vp, vp, sz, ctypes.POINTER(sz)]),
         "hfv_verify_macinputs": (i32, [vp, vp, vp, vp, sz, vp, vp]),
         "hfv_verdict_counters": (i32, [vp, vp, sz, sz, vp, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
@@ -396,6 +399,12 @@ class Ctx:
                 "consumer_busy_s": st.consumer_busy_s}
 
     @staticmethod
+    def debug_publish_delay(us):
+        """Test-only: every key/table publish copy waits behind a `us`-microsecond spin kernel on
+        its stream (0 = off)."""
+        _check(lib().hfv_debug_publish_delay(ctypes.c_uint32(us)))
+
+    @staticmethod
     def debug_br_grid(blocks):
         """Test-only: cap k_br_process launches at `blocks` blocks (0 = default geometry)."""
         _check(lib().hfv_debug_br_grid(ctypes.c_uint(blocks)))
@@ -700,6 +709,29 @@ def keymap_update(path: str, index: int, hop_key_bytes: bytes):
 
 def keymap_erase(path: str, index: int):
     _check(lib().hfv_keymap_erase(path.encode(), index))
+
+
+KEYMAP_SLOTS, KEYMAP_HASH8 = 0, 1
+
+
+def keymap_create(path: str, mode=KEYMAP_SLOTS):
+    _check(lib().hfv_keymap_create_mode(path.encode(), mode))
+
+
+def keymap_mode(path: str) -> int:
+    rc = lib().hfv_keymap_mode(path.encode())
+    _check(min(rc, 0))
+    return rc
+
+
+def keymap_list(path: str):
+    """Every entry of the map, index ascending: [(index, 192-byte hop_key)]."""
+    cap = MAX_KEYS + 8
+    idx = (ctypes.c_uint32 * cap)()
+    keys = ctypes.create_string_buffer(192 * cap)
+    n = ctypes.c_size_t(0)
+    _check(lib().hfv_keymap_list(path.encode(), idx, keys, cap, ctypes.byref(n)))
+    return [(int(idx[i]), keys.raw[192 * i:192 * i + 192]) for i in range(min(n.value, cap))]
 
 
 def keymap_read(path: str):

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-r03_fence}
 mkdir -p $OUT
-T="tests/test_gpu_parity.py::test_key_publish_visible_on_other_streams tests/test_gpu_loop.py::test_loop_single_block_chunks"
+T="tests/test_gpu_parity.py::test_key_publish_visible_on_other_streams tests/test_gpu_loop.py::test_loop_single_block_chunks tests/test_gpu_loop.py::test_loop_publish_races_second_stream"
 HFV_LIB=scion-xdp-br_amd/lib/libscionhfv_nofence.so timeout -k 10 300 python -u -m pytest $T -v --timeout 120 \
     --timeout-method thread -p no:cacheprovider > $OUT/nofence.log 2>&1
 rc=$?

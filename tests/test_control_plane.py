@@ -63,6 +63,54 @@ def test_cli_matches_br_loader_semantics(pin_dir):
     assert bad.returncode != 0 and "Usage" in bad.stderr
 
 
+def test_keymap_hash8_semantics(pin_dir):
+    """the reference's mac_key_map is a BPF hash map with a u32 index and at most
+    8 entries (maps.h:60-67).  A map in HASH8 mode (what hfv-loader creates) takes any u32
+    index and refuses a 9th new one as bpf_map_update_elem does, while an update of an existing
+    index still succeeds; the data plane's view (hfv_keymap_read) is the slots < 256."""
+    path = hfv.keymap_path("br-h8")
+    hfv.keymap_create(path, hfv.KEYMAP_HASH8)
+    assert hfv.keymap_mode(path) == hfv.KEYMAP_HASH8
+    hk = [orc.hop_key(bytes([65 + i]) * 16) for i in range(10)]
+    idx = [0, 300, 7, 4294967295, 255, 256, 1000, 3]
+    for i, k in zip(idx, hk):
+        hfv.keymap_update(path, i, k)
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_update(path, 12, hk[8])          # 9th new index: map full
+    hfv.keymap_update(path, 300, hk[9])             # existing index: BPF_ANY update
+    got = hfv.keymap_list(path)
+    assert [i for i, _ in got] == sorted(idx)
+    assert dict(got)[300] == hk[9] and dict(got)[4294967295] == hk[3]
+    assert sorted(hfv.keymap_read(path)) == [0, 3, 7, 255]   # what the data plane sees
+    hfv.keymap_erase(path, 4294967295)
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_erase(path, 4294967295)          # erase of a missing element fails
+    hfv.keymap_update(path, 12, hk[8])              # room again
+    assert len(hfv.keymap_list(path)) == 8
+    # a SLOTS map keeps the 0..255 range and no entry cap
+    sp = hfv.keymap_path("br-slots")
+    for k in range(20):
+        hfv.keymap_update(sp, k, hk[k % 10])
+    assert hfv.keymap_mode(sp) == hfv.KEYMAP_SLOTS and len(hfv.keymap_list(sp)) == 20
+    with pytest.raises(hfv.HfvError):
+        hfv.keymap_update(sp, 300, hk[0])
+
+
+def test_cli_key_index_semantics(pin_dir):
+    """`hfv-loader key add` creates the reference's map type: any u32 index, 8 entries."""
+    if not os.path.exists(LOADER):
+        pytest.skip("hfv-loader not built")
+    env = dict(os.environ)
+    for i in (0, 300, 5, 70000, 1, 2, 3, 4):
+        assert run("key", "add", "br-cli", str(i), "MTExMTExMTExMTExMTExMQ==", env=env).returncode == 0
+    bad = run("key", "add", "br-cli", "9", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert bad.returncode != 0 and "Update failed" in bad.stderr
+    lines = run("key", "list", "br-cli", env=env).stdout.split("\n")
+    assert [ln.split()[0] for ln in lines if ln] == ["0", "1", "2", "3", "4", "5", "300", "70000"]
+    assert run("key", "remove", "br-cli", "70000", env=env).returncode == 0
+    assert run("key", "add", "br-cli", "9", "MTExMTExMTExMTExMTExMQ==", env=env).returncode == 0
+
+
 def test_statsmap_and_watch(pin_dir):
     """Pinned port_stats_map + `hfv-loader watch <br> <iface>` (br_loader.cpp:162-180,
     stats.cpp:80-144): counters add up across writers; watch prints the stats.cpp table."""

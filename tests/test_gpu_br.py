@@ -116,6 +116,46 @@ def test_large_batch_mixed_sizes(gpu_ctx):
     _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[1])
 
 
+@pytest.mark.parametrize("hf_check", [True, False], ids=["hf_check", "hf_check_off"])
+def test_bench_batch_full_size_bit_exact(gpu_ctx, hf_check):
+    """the batch the config-4 bench times -- 2^20 frames in 2 KiB slots,
+    i.e. 16384 tiles, every one of the 256 x 16 waves running 4 of them -- compared with the
+    oracle byte for byte (every slot byte), with action, verdict, egress and the counters
+    (xdp.c:250-283 over the whole batch)."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n = 1 << 20
+    tmpl, tid, lens, ifidx, n_good = bench.br_batch(n, 0)
+    frames = tmpl[tid]                                     # n x 2 KiB
+    cfg = T.br_config("br1")
+    want = frames.copy()
+    oa, ov, oe, os_ = orc.br_process(want, lens, ifidx, cfg, orc.hop_key(T.KEYS[1]), hf_check=hf_check)
+    gpu_ctx.br_set_config(cfg)
+    gpu_ctx.key_add(0, T.KEYS[1])
+    gpu_ctx.br_set_hf_check(hf_check)
+    d = torch.from_numpy(frames).cuda()
+    dl = torch.from_numpy(lens.view(np.int16)).cuda()
+    di = torch.from_numpy(ifidx.view(np.int32)).cuda()
+    a = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    v = torch.zeros_like(a)
+    e = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(64 * 2 * 11, dtype=torch.int64, device="cuda")
+    gpu_ctx.br_process(d, bench.BR_SLOT, dl, di, n, a, v, e, st)
+    torch.cuda.synchronize()
+    ga, gv, ge = a.cpu().numpy(), v.cpu().numpy(), e.cpu().numpy()
+    bad = np.nonzero((ga != oa) | (gv != ov) | (ge != oe))[0]
+    assert bad.size == 0, (bad[:8], ga[bad[:4]], oa[bad[:4]], gv[bad[:4]], ov[bad[:4]])
+    dw = torch.from_numpy(want).cuda()
+    rows = torch.nonzero((d != dw).any(dim=1)).flatten().cpu().numpy()
+    assert rows.size == 0, ("frame bytes differ", rows[:8])
+    assert (st.cpu().numpy().view(np.uint64).reshape(64, 2, 11) == os_).all()
+    assert int((ga == 4).sum()) == (n_good if hf_check else n)
+    gpu_ctx.br_set_hf_check(True)
+
+
 def test_stats_accumulate_and_bad_args(gpu_ctx):
     import torch
     ing_enc, egr_enc, first, ifi = T.encaps(1, 2, False)

@@ -61,6 +61,33 @@ def test_loop_matches_oracle(gpu_ctx, hf_check, dma):
 
 
 @pytest.mark.parametrize("dma", [0, 2], ids=["zero_copy", "dma_in_zc_out"])
+def test_loop_publish_races_second_stream(gpu_ctx, dma):
+    """The round-2 failure made deterministic: the table publish the loop's first chunk does on
+    its stream is held 3 ms behind a spin kernel (hfv_debug_publish_delay), so chunk 1 on the
+    loop's second stream launches while the copy of the new key and tables is still queued.
+    It must wait for that copy (the publish fence); without it every MAC of chunk 1 fails
+    against the stale key and tx falls short by one chunk (gpurun_out/r02c5)."""
+    import torch
+    recs = torch.zeros((64, 64), dtype=torch.uint8, device="cuda:0")
+    bits = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    frames = _frame_mix(97, bad_every=5)
+    want = _oracle(frames, 10007, True)
+    for wrong in (bytes(16), bytes(range(16))):   # both device tables: a wrong slot-0 key
+        gpu_ctx.key_add(0, wrong)
+        gpu_ctx.verify_records(recs, 64, bits)
+        torch.cuda.synchronize()
+    E.setup_ctx(gpu_ctx, hf_check=True)
+    hfv.Ctx.debug_publish_delay(3000)
+    try:
+        got = gpu_ctx.loop_run(frames, np.full(97, E.FRAME_LEN), 10007, rx_ifindex=E.RX_IFINDEX, slot=SLOT,
+                               chunk=1000, chunks=3, producers=2, consumers=3, digest=True, dma=dma)
+    finally:
+        hfv.Ctx.debug_publish_delay(0)
+    for k in want:
+        assert got[k] == want[k], k
+
+
+@pytest.mark.parametrize("dma", [0, 2], ids=["zero_copy", "dma_in_zc_out"])
 def test_loop_single_block_chunks(gpu_ctx, dma):
     """The round-2 failing shape, forced: each 1000-frame chunk runs as ONE 1024-thread block
     whose 16 waves are all active (hfv_debug_br_grid(1)), zero-copy on the mapped ring, fresh

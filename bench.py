@@ -154,6 +154,8 @@ class World:
         self.dry = args.dry_run
         self.backend = "gloo" if args.dry_run else args.dist_backend
         self.device = self.local if not args.same_device else 0
+        # physical GPUs in the job: a --same-device rehearsal puts every rank on GPU 0
+        self.n_gpus = 1 if args.same_device else self.size
         if not self.dry:
             torch.cuda.set_device(self.device)
             # host waits on the device spin instead of sleeping (a packet data plane polls; the
@@ -213,6 +215,35 @@ class World:
 
 
 # ---- measurement helpers -----------------------------------------------------------------------
+
+def thread_budget(W, ctx):
+    """Host threads this rank may use: the CPUs of its GPU's NUMA node (that the process may run
+    on) divided among the ranks whose GPU hangs off the same node, capped by OMP_NUM_THREADS (the
+    box's per-GPU CPU share).  At N = 8 four ranks share each node of a two-socket host, and
+    every rank runs the host legs at once."""
+    node = ctx.numa_node()
+    cpus = len(ctx.numa_cpus())
+    nodes = W.gather(node)
+    share = max(1, sum(1 for x in nodes if int(x) == node))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    budget = max(2, cpus // share)
+    if omp > 0:
+        budget = min(budget, omp)
+    return {"budget": budget, "numa_node": node, "node_cpus": cpus, "ranks_on_node": share,
+            "omp_num_threads": omp or None}
+
+
+def apply_thread_budget(args, tb):
+    """Size this rank's host pools from its budget: the staging pool of the host path
+    (HFV_HOST_THREADS, read when the pool starts) and the config-5 loop's producer / consumer
+    threads (the calling thread drives the GPU stage)."""
+    b = tb["budget"]
+    os.environ.setdefault("HFV_HOST_THREADS", str(max(1, min(8, b))))
+    tb["host_threads"] = int(os.environ["HFV_HOST_THREADS"])
+    args.loop_threads = max(1, min(args.loop_threads, (b - 1) * 2 // 3))
+    args.loop_consumers = max(1, min(args.loop_consumers, b - 1 - args.loop_threads))
+    tb["loop_producers"], tb["loop_consumers"] = args.loop_threads, args.loop_consumers
+    return tb
 
 def make_ctx(hfv, device, keysel):
     ctx = hfv.Ctx(device)
@@ -584,7 +615,7 @@ def run_br(args, W):
         "metric": "Mpkt/s full border-router per-packet path (parse + hop-field MAC verify + rewrite), "
                   "mixed 64-1500 B frames",
         "value": round(W.size * n * steps / r["el"] / 1e6, 2),
-        "unit": "Mpkt/s", "n_gpus": W.size, "steps": steps, "warmup": args.warmup,
+        "unit": "Mpkt/s", "n_gpus": W.n_gpus, "ranks": W.size, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(r["el"] / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (PTF scenario frames of the reference test topology for BR 1, 24 flows, 64-1500 B, "
@@ -614,6 +645,7 @@ def run_br_host(args, W):
     ctx = hfv.Ctx(W.device)
     ctx.key_add(0, TP.KEYS[1])
     ctx.br_set_config(TP.br_config("br1"))
+    tb = apply_thread_budget(args, thread_budget(W, ctx))
     os.sched_setaffinity(0, ctx.numa_cpus())       # this GPU's host feeder runs on its NUMA node
     tmpl, tid, lens, ifidx, n_good = br_batch(n, W.rank)
     pristine = tmpl[tid]                                   # n x 2 KiB in host memory
@@ -642,13 +674,14 @@ def run_br_host(args, W):
     result = {
         "metric": "Mpkt/s full border-router path with frames in host memory (H2D + kernel + D2H), "
                   "mixed 64-1500 B frames",
-        "value": round(W.size * n * steps / total / 1e6, 2), "unit": "Mpkt/s", "n_gpus": W.size, "steps": steps,
+        "value": round(W.size * n * steps / total / 1e6, 2), "unit": "Mpkt/s", "n_gpus": W.n_gpus, "ranks": W.size, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(total / steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (the config-4 frame mix, 2 KiB slots in registered host memory)",
         "config": {"workload": f"config 5: {n} host-resident frames per GPU through hfv_br_process_host",
                    "frames_per_gpu": n, "slot_bytes": BR_SLOT, "path": path, "numa_node": ctx.numa_node(),
                    "parallelism": f"batch-sharded x{W.size}, no collective"},
+        "host_threads": tb,
     }
     if W.rank == 0:
         print(json.dumps(result), flush=True)
@@ -742,17 +775,21 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
 
 def run_loop(args, W):
     import scion_hfv as hfv
+    c = hfv.Ctx(W.device)
+    tb = apply_thread_budget(args, thread_budget(W, c))
+    c.close()
     r = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads, args.loop_consumers,
                      args.loop_slot, args.loop_inflight, args.loop_dma)
     result = {
         "metric": "Mpkt/s config-5 loop: RX ring -> border router on the GPU -> TX/drop, 138 B frames",
-        "value": r.get("mpkts"), "unit": "Mpkt/s", "n_gpus": W.size, "steps": 1, "warmup": 1,
+        "value": r.get("mpkts"), "unit": "Mpkt/s", "n_gpus": W.n_gpus, "ranks": W.size, "steps": 1, "warmup": 1,
         "ms_per_step": round(r["seconds"] * 1e3, 3) if "seconds" in r else None, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (gen_packets.py's 1000 frames, cycled like tcpreplay --loop)",
         "config": {"workload": f"config 5: {args.loop_n} frames per GPU through hfv_loop_run as br1-ff00_0_1-2",
                    "parallelism": f"one loop per GPU x{W.size}, no collective"},
         "loop": r,
+        "host_threads": tb,
     }
     if W.rank == 0:
         print(json.dumps(result), flush=True)
@@ -763,7 +800,7 @@ def run_dry(args, W):
     x = np.arange(1 << 12, dtype=np.uint64)
     el, per_rank = W.timed(args.steps, lambda: np.bitwise_xor.reduce(x))
     if W.rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpkt/s", "n_gpus": W.size, "steps": args.steps,
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpkt/s", "n_gpus": W.n_gpus, "ranks": W.size, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
                           "data": "dry run: launcher check only, no GPU work", "config": {"workload": "dry run"},
@@ -784,6 +821,11 @@ def run_hf(args, W):
     ctx = make_ctx(hfv, W.device, keysel)
     stream = torch.cuda.current_stream().cuda_stream
     cus = torch.cuda.get_device_properties(W.device).multi_processor_count
+    tb = apply_thread_budget(args, thread_budget(W, ctx))
+    if args.same_device and W.size > 1:
+        # ranks sharing one GPU: each service grid takes its share of the CUs (one block per CU
+        # holds the CU's LDS), so the grids run side by side instead of one after the other
+        os.environ["HFV_SVC_GRID"] = str(max(1, cus // W.size))
     m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream, reps=args.svc_reps,
                    service=not args.launch_only)
     headline = "launch" if args.launch_only else args.mode
@@ -805,7 +847,7 @@ def run_hf(args, W):
         "metric": METRIC,
         "value": round(total * args.steps / elapsed / 1e6, 2),
         "unit": "Mpkt/s",
-        "n_gpus": W.size,
+        "n_gpus": W.n_gpus, "ranks": W.size,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
@@ -848,7 +890,12 @@ def run_hf(args, W):
                        "frac": round(bytes_per_batch / (m["k_mean"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "per_rank_ms": {"min": round(min(m["per_rank_s"]) * 1e3, 4), "max": round(max(m["per_rank_s"]) * 1e3, 4),
                         "all": [round(x * 1e3, 4) for x in m["per_rank_s"]]},
+        "host_threads": tb,
     }
+    if args.same_device:
+        result["same_device"] = {"ranks": W.size, "physical_gpus": 1,
+                                 "service_grid_blocks": os.environ.get("HFV_SVC_GRID"),
+                                 "note": "launcher rehearsal: every rank on GPU 0"}
     recs0, bits0 = m["batches"][0], m["bitmaps"][0]
     extras = W.size == 1 and not args.no_extras
 
@@ -989,7 +1036,8 @@ def main():
     ap.add_argument("--no-register", action="store_true", help="br-host: leave the ring unregistered (DMA windows)")
     ap.add_argument("--no-hf-check", action="store_true", help="br: the ENABLE_HF_CHECK=OFF router")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
-    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (launcher rehearsal on 1 GPU; gloo)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on GPU 0 (launcher rehearsal on 1 GPU; gloo; service grids of cus/ranks blocks)")
     ap.add_argument("--dry-run", action="store_true", help="launcher check: gloo ranks, no GPU work")
     args = ap.parse_args()
     if args.steps is None:
@@ -997,8 +1045,7 @@ def main():
     if args.warmup is None:
         args.warmup = {"hf": 20, "br": 3, "br-host": 1, "loop": 1}[args.workload]
     if args.same_device:
-        args.dist_backend = "gloo"
-        args.launch_only = True
+        args.dist_backend = "gloo"   # one GPU: RCCL would not place two ranks on it
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))           # before anything touches a GPU
     W = World(args)

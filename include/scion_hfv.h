@@ -314,6 +314,19 @@ int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg);
  * of border_router, path_processing.h:43-57 / xdp.c:259-274); default on.  Takes effect
  * for batches enqueued afterwards; survives hfv_br_set_config. */
 int hfv_br_set_hf_check(hfv_ctx *ctx, int enable);
+/* The reference's other build options (br/CMakeLists.txt:5-7, common.h:31-33), as a runtime
+ * switch of the router: HFV_BR_NO_IPV4 / HFV_BR_NO_IPV6 compile that case of parse_underlay out
+ * (parser.h:60,81: such frames fall to `default`, VERDICT_NOT_SCION, XDP_PASS), HFV_BR_NO_SCION_PATH
+ * the standard SCION path type (parser.h:140: VERDICT_NOT_IMPLEMENTED).  Default 0: all built.
+ * -EINVAL (tables unchanged) if the installed tables hold an address of a switched-off family,
+ * which br-loader rejects (maps.cpp:68-80 "Border router configuration contains IPv4 address,
+ * but IPv4 support is deactivated."); hfv_br_set_config checks the same against the options. */
+#define HFV_BR_NO_IPV4 1u
+#define HFV_BR_NO_IPV6 2u
+#define HFV_BR_NO_SCION_PATH 4u
+int hfv_br_set_build_options(hfv_ctx *ctx, uint32_t disabled);
+/* That check alone (for a loader): 0, or -EINVAL with br-loader's message in hfv_last_error(). */
+int hfv_br_config_check_options(const struct hfv_br_config *cfg, uint32_t disabled);
 /* ---- control plane: br-loader's configuration path ---------------------------------------
  * loadConfig + initializeMaps (br/src/config.cpp:212-262, maps.cpp:91-200, called by attachBr,
  * br_loader.cpp:88-151) for C hosts: the br-loader TOML file (`self`, `topology`,
@@ -351,6 +364,8 @@ int hfv_br_load_config(hfv_ctx *ctx, const char *toml_path, const struct hfv_br_
  * whole tables (seqlock). */
 int hfv_brconfig_path(const char *br, char *out, size_t len);
 int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg);
+/* The same with the router's build options (HFV_BR_NO_*), which an attached ctx adopts. */
+int hfv_brconfig_publish_opts(const char *path, const struct hfv_br_config *cfg, uint32_t disabled);
 int hfv_brconfig_read(const char *path, struct hfv_br_config *cfg);
 /* `hfv-loader detach`: marks the pinned tables detached (the file stays, so data planes that
  * attached it see the change): from their next batch an attached ctx passes every frame

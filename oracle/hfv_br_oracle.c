@@ -59,6 +59,7 @@ typedef struct {
     uint8_t v6_hop;
     uint16_t udp_dst, udp_src;
     uint32_t path_type;
+    uint32_t feat_off;   /* ORC_BR_NO_*: the build options switched off */
     uint32_t h_meta, curr_inf, curr_hf;
     uint16_t seg_id[2];
     uint32_t segment_switch, seg0, seg1, seg2, num_inf, num_hf;
@@ -100,7 +101,9 @@ static long parse_underlay(pkt_t *k, long off)
     memcpy(k->eth_dst, k->p + k->eth, 6);
     memcpy(k->eth_src, k->p + k->eth + 6, 6);
     uint16_t proto = l16(k->p + k->eth + 12);
-    if (proto == sw16(0x0800)) {
+    /* ENABLE_IPV4 / ENABLE_IPV6 off (br/CMakeLists.txt:5-6): that case of the switch is compiled
+     * out (parser.h:60, 81), so the frame falls to `default` -- NOT_SCION, XDP_PASS */
+    if (proto == sw16(0x0800) && !(k->feat_off & ORC_BR_NO_IPV4)) {
         k->ip = off;
         off += 20;
         if (off > k->len) return -1;
@@ -117,7 +120,7 @@ static long parse_underlay(pkt_t *k, long off)
         memset(k->v6_src, 0, sizeof k->v6_src);
         k->v6_hop = 0;
         if (ip[9] != 17) return -1;
-    } else if (proto == sw16(0x86DD)) {
+    } else if (proto == sw16(0x86DD) && !(k->feat_off & ORC_BR_NO_IPV6)) {
         k->ip = off;
         off += 40;
         if (off > k->len) return -1;
@@ -190,7 +193,8 @@ static long parse_scion(pkt_t *k, long off)
     off += 8 + 4 * ((haddr >> 2) & 0x2) + 4 * ((haddr >> 6) & 0x2);
     if (off > k->len) return -1;
     k->path_type = sc[8];
-    if (k->path_type == 1) return parse_scion_path(k, off);
+    /* ENABLE_SCION_PATH off (br/CMakeLists.txt:7): no case for the standard path (parser.h:140) */
+    if (k->path_type == 1 && !(k->feat_off & ORC_BR_NO_SCION_PATH)) return parse_scion_path(k, off);
     k->verdict = V_NOT_IMPLEMENTED;
     return -1;
 }
@@ -545,9 +549,9 @@ static int border_router(pkt_t *k, int hf_check)
     return record(k, verdict);
 }
 
-void orc_br_process_ex(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
-                       const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
-                       int32_t *egress_ifindex, uint64_t *stats, int hf_check)
+void orc_br_process_feat(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                         const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                         int32_t *egress_ifindex, uint64_t *stats, int hf_check, uint32_t feat_off)
 {
     for (size_t i = 0; i < n; ++i) {
         pkt_t k;
@@ -559,11 +563,20 @@ void orc_br_process_ex(uint8_t *pkts, size_t slot, const uint16_t *len, const ui
         k.key = key0;
         k.stats = stats;
         k.last_verdict = 0;
+        k.feat_off = feat_off;
         int a = border_router(&k, hf_check);
         action[i] = (uint8_t)a;
         verdict[i] = (uint8_t)k.last_verdict;
         egress_ifindex[i] = k.egress_ifindex;
     }
+}
+
+void orc_br_process_ex(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                       const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                       int32_t *egress_ifindex, uint64_t *stats, int hf_check)
+{
+    orc_br_process_feat(pkts, slot, len, ingress_ifindex, n, cfg, key0, action, verdict, egress_ifindex, stats, hf_check,
+                        0);
 }
 
 void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,

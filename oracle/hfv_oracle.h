@@ -91,6 +91,14 @@ void orc_gen_records(uint8_t *recs, size_t stride, size_t n, uint64_t seed, uint
 void orc_br_process(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                     const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
                     int32_t *egress_ifindex, uint64_t *stats);
+/* feat_off: build options switched off (br/CMakeLists.txt:5-7) -- ENABLE_IPV4, ENABLE_IPV6,
+ * ENABLE_SCION_PATH; the same bits as HFV_BR_NO_* in include/scion_hfv.h. */
+#define ORC_BR_NO_IPV4 1u
+#define ORC_BR_NO_IPV6 2u
+#define ORC_BR_NO_SCION_PATH 4u
+void orc_br_process_feat(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
+                         const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,
+                         int32_t *egress_ifindex, uint64_t *stats, int hf_check, uint32_t feat_off);
 /* hf_check = 0: the ENABLE_HF_CHECK=OFF router (no hop-field MAC check). */
 void orc_br_process_ex(uint8_t *pkts, size_t slot, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                        const void *cfg, const orc_hop_key *key0, uint8_t *action, uint8_t *verdict,

@@ -298,6 +298,42 @@ struct LdsKey {              // per-lane slot from the LDS copy of the table
     __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
 };
 
+// Per-lane slot with the packet's key rows gathered from the slot-major table
+// (DevKeyTable::gather) into VGPRs: LDS serves only the round tables, so the per-interface
+// key rows cost no LDS cycles and no bank conflicts (the LDS copy of the round-major image,
+// LdsKey, read 11 random 16 B rows per packet: ~3 conflict cycles each).  issue() starts the
+// loads (global address space: vmcnt only, never lgkmcnt); the rounds wait for each row where
+// they use it.  Valid bits come from the LDS copy s_valid.
+struct GatherKey {
+    uint4 k[11];
+    uint32_t slot;
+    __device__ __forceinline__ void issue(const DevKeyTable *tab, uint32_t s)
+    {
+        slot = s;
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(1))) v4 *G4;
+        const G4 g = (G4)(tab->gather[s]);   // generic -> global address space
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+            const v4 x = g[j];
+            k[j] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    }
+    __device__ __forceinline__ uint4 row(int r) const { return r == 0 ? k[0] : r == 11 ? k[1] : k[r]; }
+    template <int TAB>
+    __device__ __forceinline__ uint4 rk(int r) const
+    {
+        static_assert(TAB == 4, "gathered rows are not rotated");
+        return k[r];
+    }
+    __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
+};
+
+__device__ __forceinline__ void fill_valid(const DevKeyTable *tab)
+{
+    if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
+}
+
 // Tag words 0..1 for a record-derived macinput w[] (bytes 0,1,8,14,15 zero).
 template <int TAB, class K>
 __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &key, const Lane &l, uint32_t &t0,

@@ -209,6 +209,7 @@ struct hfv_ctx {
     hipEvent_t tev[2] = {nullptr, nullptr};
     // router tables for hfv_br_process (published with the key table)
     DevBrConfig br{};
+    hfv_br_config cfg_src{};   // the tables as installed (checked against the build options)
     // windowed host path (hfv_br_process_host): per-stream device/pinned chunk buffers
     size_t brh_win_cap = 0;               // bytes per frame the device windows hold
     uint8_t *brh_dwin[2] = {nullptr, nullptr};
@@ -297,8 +298,8 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         uint32_t seq = brcfg_seq(ctx->brmap);
         if (seq != ctx->brmap_seq) {
             hfv_br_config cfg;
-            uint32_t detached = 0;
-            ctx->brmap_seq = brcfg_snapshot(ctx->brmap, &cfg, &detached);
+            uint32_t detached = 0, feat_off = 0;
+            ctx->brmap_seq = brcfg_snapshot(ctx->brmap, &cfg, &detached, &feat_off);
             if (br_config_check(&cfg) != 0)   // a corrupt or foreign file: keep the tables in use
                 return fail(-EINVAL, "attached router config holds counts past the fixed capacity; "
                                      "previous tables kept");
@@ -306,6 +307,7 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
             compile_br_config(&cfg, &ctx->br);
             ctx->br.hf_check_off = off;
             ctx->br.detached = detached;
+            ctx->br.feat_off = feat_off & (HFV_BR_NO_IPV4 | HFV_BR_NO_IPV6 | HFV_BR_NO_SCION_PATH);
             ctx->dirty = true;
         }
     }
@@ -318,6 +320,12 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
             if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) compile_dev_key(&ctx->shadow[k], dk);
             else memset(dk, 0, sizeof dk);
             for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->keys.rows[r][k], dk + 4 * r, 16);
+            uint32_t(*g)[4] = ctx->host_img->keys.gather[k];   // slot-major, rows 2..9 unrotated
+            memcpy(g[0], dk, 16);
+            memcpy(g[1], dk + 44, 16);
+            for (int r = 2; r < 10; ++r)
+                for (int c = 0; c < 4; ++c) g[r][c] = (dk[4 * r + c] << 16) | (dk[4 * r + c] >> 16);
+            memcpy(g[10], dk + 40, 16);
         }
         memcpy(ctx->host_img->keys.valid, ctx->valid, sizeof ctx->valid);
         ctx->host_img->br = ctx->br;
@@ -794,12 +802,16 @@ int hfv_verdict_counters(hfv_ctx *ctx, const void *recs, size_t stride, size_t n
 int hfv_br_set_config(hfv_ctx *ctx, const struct hfv_br_config *cfg)
 {
     if (!ctx || !cfg) return fail(-EINVAL, "null argument");
+    if (br_config_check(cfg) == 0 && ctx->br.feat_off && hfv_br_config_check_options(cfg, ctx->br.feat_off))
+        return -EINVAL;   // an address of a family the router is built without (br-loader's error)
     if (br_config_check(cfg))
         return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
                     HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
-    const uint32_t off = ctx->br.hf_check_off;
+    const uint32_t off = ctx->br.hf_check_off, feat = ctx->br.feat_off;
     compile_br_config(cfg, &ctx->br);
     ctx->br.hf_check_off = off;
+    ctx->br.feat_off = feat;
+    ctx->cfg_src = *cfg;
     ctx->dirty = true;
     brcfg_close(ctx->brmap);   // explicit tables replace an attached pinned config
     ctx->brmap = nullptr;
@@ -824,6 +836,15 @@ int hfv_ctx_attach_brconfig(hfv_ctx *ctx, const char *path)
     brcfg_close(ctx->brmap);
     ctx->brmap = m;
     ctx->brmap_seq = 0xffffffffu;   // loaded at the next batch boundary
+    return 0;
+}
+
+int hfv_br_set_build_options(hfv_ctx *ctx, uint32_t disabled)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (hfv_br_config_check_options(&ctx->cfg_src, disabled)) return -EINVAL;
+    ctx->br.feat_off = disabled;
+    ctx->dirty = true;
     return 0;
 }
 

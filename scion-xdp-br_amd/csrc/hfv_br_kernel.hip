@@ -256,7 +256,8 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
     int off = 14;
     if (beyond(k, off)) return -1;
     uint32_t proto = rd16(k, 12);
-    if (proto == 0x0008u) {   // ETH_P_IP, network order
+    // HFV_BR_NO_IPV4 / _IPV6: the reference built without that case (parser.h:60,81) -> default
+    if (proto == 0x0008u && !(s_br.feat_off & HFV_BR_NO_IPV4)) {   // ETH_P_IP, network order
         k.ip = off;
         off += 20;
         if (beyond(k, off)) return -1;
@@ -265,7 +266,7 @@ __device__ __forceinline__ int parse_underlay(BrFrame &k)
         if (skip < 0 || skip > 40) return -1;
         off += skip;
         if (rd8(k, k.ip + 9) != 17u) return -1;
-    } else if (proto == 0xdd86u) {   // ETH_P_IPV6
+    } else if (proto == 0xdd86u && !(s_br.feat_off & HFV_BR_NO_IPV6)) {   // ETH_P_IPV6
         k.ip = off;
         off += 40;
         if (beyond(k, off)) return -1;
@@ -320,7 +321,8 @@ __device__ __forceinline__ int parse_scion(BrFrame &k, int off)
     uint32_t haddr = rd8(k, sc + 9);
     off += 8 + 4 * (int)((haddr >> 2) & 0x2u) + 4 * (int)((haddr >> 6) & 0x2u);   // SC_GET_DL/SL, scion.h:49-52
     if (beyond(k, off)) return -1;
-    if (rd8(k, sc + 8) == 1u) return parse_scion_path(k, off);   // path_type SCION
+    // path_type SCION, unless built without ENABLE_SCION_PATH (parser.h:140)
+    if (rd8(k, sc + 8) == 1u && !(s_br.feat_off & HFV_BR_NO_SCION_PATH)) return parse_scion_path(k, off);
     k.verdict = V_NOT_IMPLEMENTED;
     return -1;
 }

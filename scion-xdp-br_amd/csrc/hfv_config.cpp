@@ -783,7 +783,8 @@ struct BrcfgFile {
     uint32_t version;
     uint32_t seq;          // seqlock: odd while a writer updates the tables
     uint32_t detached;     // 1: `hfv-loader detach` -- attached data planes pass every frame
-    uint8_t reserved[44];
+    uint32_t feat_off;     // HFV_BR_NO_*: build options the attached router runs without
+    uint8_t reserved[40];
     hfv_br_config cfg;
 };
 static_assert(sizeof(BrcfgFile) == 64 + sizeof(hfv_br_config), "pinned file layout unchanged");
@@ -807,7 +808,7 @@ static int mkdir_parents(const char *path)
 
 // Consistent snapshot of a pinned br_config mapping (tables and detached flag); returns its
 // (even) seq.
-uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached)
+uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached, uint32_t *feat_off)
 {
     const BrcfgFile *f = (const BrcfgFile *)mapping;
     for (;;) {
@@ -815,9 +816,11 @@ uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detac
         if (s0 & 1u) { usleep(10); continue; }
         memcpy(out, &f->cfg, sizeof *out);
         const uint32_t d = __atomic_load_n(&f->detached, __ATOMIC_RELAXED);
+        const uint32_t fo = __atomic_load_n(&f->feat_off, __ATOMIC_RELAXED);
         std::atomic_thread_fence(std::memory_order_acquire);
         if (__atomic_load_n(&f->seq, __ATOMIC_ACQUIRE) == s0) {
             if (detached) *detached = d;
+            if (feat_off) *feat_off = fo;
             return s0;
         }
     }
@@ -906,7 +909,35 @@ int hfv_brconfig_path(const char *br, char *out, size_t len)
 
 int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg)
 {
+    return hfv_brconfig_publish_opts(path, cfg, 0);
+}
+
+int hfv_br_config_check_options(const struct hfv_br_config *cfg, uint32_t disabled)
+{
+    if (!cfg) return fail(-EINVAL, "null argument");
+    if (disabled & ~(HFV_BR_NO_IPV4 | HFV_BR_NO_IPV6 | HFV_BR_NO_SCION_PATH)) return fail(-EINVAL, "unknown build option");
+    if (br_config_check(cfg)) return fail(-EINVAL, "router table larger than the fixed capacity");
+    // the tables initializeMaps stores addresses into (maps.cpp:91-200): ingress keys, links and
+    // siblings, internal interfaces
+    auto off = [&](uint32_t family) {
+        return (family == HFV_AF_INET && (disabled & HFV_BR_NO_IPV4)) || (family == HFV_AF_INET6 && (disabled & HFV_BR_NO_IPV6));
+    };
+    bool bad4 = false, bad6 = false;
+    auto note = [&](uint32_t family) {
+        if (off(family)) (family == HFV_AF_INET ? bad4 : bad6) = true;
+    };
+    for (uint32_t i = 0; i < cfg->n_ingress; ++i) note(cfg->ingress[i].family);
+    for (uint32_t i = 0; i < cfg->n_egress; ++i) note(cfg->egress[i].family);
+    for (uint32_t i = 0; i < cfg->n_int_ifaces; ++i) note(cfg->int_ifaces[i].family);
+    if (bad4) return fail(-EINVAL, "Border router configuration contains IPv4 address, but IPv4 support is deactivated.");
+    if (bad6) return fail(-EINVAL, "Border router configuration contains IPv6 address, but IPv6 support is deactivated.");
+    return 0;
+}
+
+int hfv_brconfig_publish_opts(const char *path, const struct hfv_br_config *cfg, uint32_t disabled)
+{
     if (!path || !cfg) return fail(-EINVAL, "null argument");
+    if (hfv_br_config_check_options(cfg, disabled)) return -EINVAL;
     if (br_config_check(cfg))
         return fail(-EINVAL, "router table larger than the fixed capacity (%d interfaces, %d routes, %d tx ports)",
                     HFV_BR_MAX_IFACES, HFV_BR_MAX_ROUTES, HFV_BR_MAX_TXPORTS);
@@ -937,6 +968,7 @@ int hfv_brconfig_publish(const char *path, const struct hfv_br_config *cfg)
     std::atomic_thread_fence(std::memory_order_release);
     f->cfg = *cfg;
     __atomic_store_n(&f->detached, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&f->feat_off, disabled, __ATOMIC_RELAXED);
     __atomic_store_n(&f->seq, f->seq + 1, __ATOMIC_RELEASE);   // even: published
     msync(m, sizeof(BrcfgFile), MS_SYNC);
     munmap(m, sizeof(BrcfgFile));

@@ -20,10 +20,18 @@ void compile_dev_key(const hop_key *hk, uint32_t dk[4 * kDevKeyRows]);
 
 // Device key table as the kernels see it: dev keys in round-major order
 // [kDevKeyRows][HFV_MAX_KEYS] x 16 B, followed by the 256-bit valid bitmap.
+constexpr int kGatherRows = 16;   // 11 used: one slot = 256 B = two 128 B lines
 struct DevKeyTable {
     uint32_t rows[kDevKeyRows][HFV_MAX_KEYS][4];
     uint32_t valid[8];
+    uint32_t pad_[56];   // gather[] on a 256 B boundary
+    // Slot-major copy for the kernels that gather each packet's key rows into VGPRs
+    // (per-interface keys with the 4-table layout, hfv_aes_dev.h GatherKey): gather[slot][j],
+    // j = 0: row 0 (rk0 ^ K1), 1: row 11 (folded round 1), 2..9: rounds 2..9 NOT rotated,
+    // 10: row 10 (last round); 11..15 unused.
+    uint32_t gather[HFV_MAX_KEYS][kGatherRows][4];
 };
+static_assert(offsetof(DevKeyTable, gather) % 256 == 0, "gather rows on 256 B boundaries");
 
 // Router tables as the config-4 kernel sees them (compiled from struct hfv_br_config by
 // hfv_br_set_config).  Addresses/ports keep the BPF code's little-endian view of wire bytes
@@ -61,7 +69,8 @@ struct DevBrConfig {
     uint32_t n_int, n_ing, n_egr, n_routes;
     uint32_t hf_check_off;   // 1: the ENABLE_HF_CHECK=OFF router (hfv_br_set_hf_check)
     uint32_t detached;       // 1: the attached pinned config was detached -- every frame passes
-    uint32_t pad_[2];
+    uint32_t feat_off;       // HFV_BR_NO_*: the reference build options switched off
+    uint32_t pad_[1];
     uint32_t tx_bits[HFV_BR_MAX_TXPORTS / 32];
     DevBrIntIface int_ifaces[HFV_BR_MAX_IFACES];
     DevBrIngress ingress[HFV_BR_MAX_IFACES];
@@ -182,7 +191,7 @@ int keymap_create(const char *path, uint32_t mode);   // empty map (header only)
 int brcfg_open_ro(const char *path, const void **mapping);
 void brcfg_close(const void *mapping);
 uint32_t brcfg_seq(const void *mapping);
-uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached);
+uint32_t brcfg_snapshot(const void *mapping, hfv_br_config *out, uint32_t *detached, uint32_t *feat_off = nullptr);
 int br_config_check(const hfv_br_config *cfg);
 void keymap_close(const void *mapping);
 uint32_t keymap_seq(const void *mapping);

@@ -182,6 +182,24 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
     }
 }
 
+// Per-interface keys gathered into VGPRs (GatherKey) with the 4-table LDS layout: an internal
+// key-selection value for the kernels' template argument (the host still says
+// HFV_KEYSEL_IFID; the slot rule is the same, xdp.c:151-157).
+constexpr int kKeyselGather = 2;
+
+// One tile with the per-lane key rows already issued (GatherKey::issue): the verdict ballot.
+template <int TAB>
+__device__ __forceinline__ uint64_t verify_tile_gather(const RecWords &r, uint64_t t, uint64_t n, uint32_t lane,
+                                                       const Lane &l, const GatherKey &key)
+{
+    uint32_t w[4];
+    rec_macinput(r, w);
+    uint32_t t0, t1;
+    cmac48_macinput<TAB>(w, key, l, t0, t1);
+    const bool pass = t * 64 + lane < n && key.ok() && rec_tag_matches(r, t0, t1);
+    return __ballot(pass);
+}
+
 // STAMP = 1 is a diagnostic build: lane 0 of every wave records s_memrealtime (100 MHz,
 // chip-wide) at entry, after the table fill, after each of its first 10 tiles (12 in the
 // static variant) and at exit into stamps[wave * 16 + k]; the dynamic variant also records
@@ -965,6 +983,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
         if (!relay) fill_keys(tab, nthr);
+    } else if constexpr (KEYSEL == kKeyselGather) {
+        fill_valid(tab);
     }
     __syncthreads();
     if (relay) {   // no barrier follows: the block's other waves go on without it
@@ -973,7 +993,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     }
     const Lane l = lane_bases();
     // KEYSEL_ZERO with slot 0 empty: every packet fails closed (xdp.c:83-84)
-    const bool keyok = KEYSEL == HFV_KEYSEL_IFID || ukey.ok;
+    const bool keyok = KEYSEL != HFV_KEYSEL_ZERO || ukey.ok;
     const UniformKey *ukp = KEYSEL == HFV_KEYSEL_ZERO ? &ukey : nullptr;
 
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // diagnostics: shader clock over the grid's life
@@ -1045,6 +1065,10 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
             dc_k = fl_k;
             flush = false;
         }
+        // per-interface keys: this tile's key rows, issued BEFORE the next tile's record loads
+        // (vmcnt retires in order: a row wait must not also wait for those HBM loads)
+        GatherKey gk;
+        if constexpr (KEYSEL == kKeyselGather) gk.issue(tab, rec_key_slot(rc));
         const uint32_t g = wave_uniform(gq);
         gq = claim();
         SvcTile nx;
@@ -1053,7 +1077,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         RecWords rn = load_tile(nx, lane, inf_off, hf_off);
         prof.mark(1);
         uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
-        if (keyok) {
+        if constexpr (KEYSEL == kKeyselGather) {
+            ballot = verify_tile_gather<TAB>(rc, cur.tile, cur.n, lane, l, gk);
+        } else if (keyok) {
             RecWords c1[1] = {rc};
             verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
         }
@@ -1126,7 +1152,12 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
                           uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid_out)
 {
-    auto k = keysel == HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_IFID, 2> : k_verify_service<HFV_KEYSEL_ZERO, 4>;
+    // per-interface keys: key rows gathered into VGPRs beside the 4 LDS round tables (default),
+    // or HFV_SVC_IFID_LDS=1 for the round-2 layout (key image in LDS, 2 tables + rotation)
+    static const bool ifid_lds = getenv("HFV_SVC_IFID_LDS") && atoi(getenv("HFV_SVC_IFID_LDS"));
+    auto k = keysel != HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_ZERO, 4>
+             : ifid_lds               ? k_verify_service<HFV_KEYSEL_IFID, 2>
+                                      : k_verify_service<kKeyselGather, 4>;
     const char *ge = getenv("HFV_SVC_GRID");   // experiments only: fewer blocks than CUs
     unsigned grid = ge && atoi(ge) > 0 && atoi(ge) < g.num_cus ? (unsigned)atoi(ge) : (unsigned)g.num_cus;
     if (grid > kSvcMaxBlocks) grid = kSvcMaxBlocks;
@@ -1258,6 +1289,14 @@ __global__ __launch_bounds__(256) void k_expand_keys(const uint4 *__restrict__ r
         p[1] = w[5] ^ tg(2, k0[3] >> 16);
         p[2] = w[6] ^ tg(0, k0[2]);
         p[3] = w[7] ^ tg(1, k0[0] >> 8);
+        uint32_t(*g)[4] = tab->gather[slot];   // slot-major copy (hfv_internal.h)
+        for (int c = 0; c < 4; ++c) {
+            g[0][c] = k0[c];
+            g[1][c] = p[c];
+            g[10][c] = w[40 + c];
+        }
+        for (int r = 2; r < 10; ++r)
+            for (int c = 0; c < 4; ++c) g[r][c] = w[4 * r + c];
         atomicOr(&tab->valid[slot >> 5], 1u << (slot & 31));
     }
 }

@@ -43,7 +43,8 @@ static void print_usage()
             "                  key remove <br> <index>\n"
             "                  key list <br>\n"
             "       hfv-loader watch <br> <iface> [seconds]\n"
-            "       hfv-loader attach <config> [--key-slots] [--route <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]]...\n"
+            "       hfv-loader attach <config> [--key-slots] [--no-ipv4] [--no-ipv6] [--no-scion-path]\n"
+            "                         [--route <prefix>/<len>,<iface>,<smac>,<dmac>[,<ret>]]...\n"
             "                  detach <br>\n");
 }
 
@@ -267,6 +268,7 @@ static int attach(int argc, char **argv)
     static struct hfv_br_next_hop hops[HFV_BR_MAX_ROUTES];
     size_t nh = 0;
     int kmode = HFV_KEYMAP_HASH8;   // the reference's mac_key_map (maps.h:60-67)
+    uint32_t disabled = 0;
     for (int i = 1; i < argc; ++i) {
         if (strcmp(argv[i], "--route") == 0 && i + 1 < argc && nh < HFV_BR_MAX_ROUTES && parse_route(argv[i + 1], &hops[nh])) {
             ++nh;
@@ -277,6 +279,10 @@ static int attach(int argc, char **argv)
             kmode = HFV_KEYMAP_SLOTS;
             continue;
         }
+        // the reference's build options switched off (br/CMakeLists.txt:5-7)
+        if (strcmp(argv[i], "--no-ipv4") == 0) { disabled |= HFV_BR_NO_IPV4; continue; }
+        if (strcmp(argv[i], "--no-ipv6") == 0) { disabled |= HFV_BR_NO_IPV6; continue; }
+        if (strcmp(argv[i], "--no-scion-path") == 0) { disabled |= HFV_BR_NO_SCION_PATH; continue; }
         fprintf(stderr, "Invalid argument: %s\n", argv[i]);
         print_usage();
         return EXIT_FAILURE;
@@ -288,6 +294,13 @@ static int attach(int argc, char **argv)
     fputs(diag, stderr);
     if (rc) return EXIT_FAILURE;
     fputs(listing, stdout);
+    fflush(stdout);
+    // initializeMaps stores every address through STORE_IPV4/6, which throw for a family the
+    // router is built without (maps.cpp:68-80); main prints "ERROR: ..." (br_loader.cpp:291-294)
+    if (hfv_br_config_check_options(&cfg, disabled) != 0) {
+        fprintf(stderr, "ERROR: %s\n", hfv_last_error());
+        return EXIT_FAILURE;
+    }
     char kpath[4096], spath[4096], cpath[4096];
     if (hfv_keymap_path(self, kpath, sizeof kpath) || hfv_statsmap_path(self, spath, sizeof spath) ||
         hfv_brconfig_path(self, cpath, sizeof cpath)) {
@@ -308,7 +321,7 @@ static int attach(int argc, char **argv)
             return EXIT_FAILURE;
         }
     }
-    if (hfv_brconfig_publish(cpath, &cfg) != 0) {
+    if (hfv_brconfig_publish_opts(cpath, &cfg, disabled) != 0) {
         fprintf(stderr, "Cannot publish router tables: %s\n", hfv_last_error());
         return EXIT_FAILURE;
     }

@@ -81,6 +81,9 @@ def lib():
         "hfv_verdict_counters": (i32, [vp, vp, sz, sz, vp, vp, vp]),
         "hfv_br_set_config": (i32, [vp, vp]),
         "hfv_br_set_hf_check": (i32, [vp, i32]),
+        "hfv_br_set_build_options": (i32, [vp, u32]),
+        "hfv_br_config_check_options": (i32, [vp, u32]),
+        "hfv_brconfig_publish_opts": (i32, [ctypes.c_char_p, vp, u32]),
         "hfv_br_config_load": (i32, [ctypes.c_char_p, vp, sz, vp, sz, vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
                                      ctypes.c_char_p, sz]),
         "hfv_br_load_config": (i32, [vp, ctypes.c_char_p, vp, sz]),
@@ -366,6 +369,11 @@ class Ctx:
     def br_set_hf_check(self, enable: bool):
         """ENABLE_HF_CHECK on/off (br/CMakeLists.txt:8): off skips the hop-field MAC check."""
         _check(lib().hfv_br_set_hf_check(self._h, 1 if enable else 0))
+
+    def br_set_build_options(self, disabled):
+        """HFV_BR_NO_IPV4 | HFV_BR_NO_IPV6 | HFV_BR_NO_SCION_PATH: the reference's build options
+        switched off (br/CMakeLists.txt:5-7)."""
+        _check(lib().hfv_br_set_build_options(self._h, disabled))
 
     def br_process(self, pkts, slot, lens, ingress_ifindex, n, action, verdict, egress_ifindex, stats=None,
                    stream=None):
@@ -682,6 +690,17 @@ def brconfig_read(path: str):
     cfg = BrConfig()
     _check(lib().hfv_brconfig_read(path.encode(), ctypes.byref(cfg)))
     return cfg
+
+
+BR_NO_IPV4, BR_NO_IPV6, BR_NO_SCION_PATH = 1, 2, 4
+
+
+def br_config_check_options(cfg, disabled):
+    _check(lib().hfv_br_config_check_options(ctypes.byref(cfg), disabled))
+
+
+def brconfig_publish_opts(path: str, cfg, disabled):
+    _check(lib().hfv_brconfig_publish_opts(path.encode(), ctypes.byref(cfg), disabled))
 
 
 def brconfig_detach(path: str):

@@ -21,13 +21,15 @@ class OracleBR:
 class GpuBR:
     """One BR instance backed by libscionhfv on the GPU (hfv_br_process)."""
 
-    def __init__(self, ctx, cfg, key0=KEYS[1], hf_check=True):
-        self.ctx, self.cfg, self.key0, self.hf_check = ctx, cfg, key0, hf_check
+    def __init__(self, ctx, cfg, key0=KEYS[1], hf_check=True, feat_off=0):
+        self.ctx, self.cfg, self.key0, self.hf_check, self.feat_off = ctx, cfg, key0, hf_check, feat_off
 
     def process(self, frames, lens, ifidx):
         import torch
         ctx = self.ctx
+        ctx.br_set_build_options(0)
         ctx.br_set_config(self.cfg)
+        ctx.br_set_build_options(self.feat_off)
         ctx.br_set_hf_check(self.hf_check)
         if self.key0 is None:
             try:

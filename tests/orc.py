@@ -145,7 +145,7 @@ def expected_pass_rule(n, seed=SEED_RECORDS, first_index=0):
 BR_STATS_SHAPE = (64, 2, 11)   # HFV_BR_STATS_IFINDEX x (bytes, packets) x HFV_BR_COUNTERS
 
 
-def br_process(frames, lens, ifidx, cfg, key0_hop_key=None, stats=None, hf_check=True):
+def br_process(frames, lens, ifidx, cfg, key0_hop_key=None, stats=None, hf_check=True, feat_off=0):
     """Oracle border router (hfv_br_oracle.c) over frames[n, slot] in place.
     Returns (action u8[n], verdict u8[n], egress i32[n], stats u64[64, 2, 11])."""
     n, slot = frames.shape
@@ -158,9 +158,9 @@ def br_process(frames, lens, ifidx, cfg, key0_hop_key=None, stats=None, hf_check
     if stats is None:
         stats = np.zeros(BR_STATS_SHAPE, dtype=np.uint64)
     key = ctypes.create_string_buffer(bytes(key0_hop_key), 192) if key0_hop_key is not None else None
-    oracle().orc_br_process_ex(_vp(frames), ctypes.c_size_t(slot), _vp(lens), _vp(ifidx), ctypes.c_size_t(n),
-                               ctypes.byref(cfg), key, _vp(action), _vp(verdict), _vp(egress), _vp(stats),
-                               ctypes.c_int(1 if hf_check else 0))
+    oracle().orc_br_process_feat(_vp(frames), ctypes.c_size_t(slot), _vp(lens), _vp(ifidx), ctypes.c_size_t(n),
+                                 ctypes.byref(cfg), key, _vp(action), _vp(verdict), _vp(egress), _vp(stats),
+                                 ctypes.c_int(1 if hf_check else 0), ctypes.c_uint32(feat_off))
     return action, verdict, egress, stats
 
 

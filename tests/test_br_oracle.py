@@ -137,6 +137,31 @@ def test_hf_check_off_forwards_bad_macs():
             assert out == ref[4]
 
 
+def test_build_options():
+    """ENABLE_IPV4 / ENABLE_IPV6 / ENABLE_SCION_PATH off (br/CMakeLists.txt:5-7): parse_underlay
+    has no case for the family (parser.h:60,81) -> NOT_SCION, XDP_PASS, frame untouched;
+    parse_scion has no case for the standard path (parser.h:140) -> NOT_IMPLEMENTED.  The loader
+    check refuses tables holding an address of a switched-off family (maps.cpp:68-80)."""
+    for v6 in (False, True):
+        ing_enc, egr_enc, first, ifi = T.encaps(1, 2, v6)
+        path = P.ptf_path("down", 1, 2, T.KEYS, seed=7, mac_fn=MAC)
+        frame = ing_enc.frame(P.scion_header(path.pack()))
+        cfg = T.br_config("br1", v6)
+        for feat, want in ((hfv.BR_NO_IPV6 if v6 else hfv.BR_NO_IPV4, (2, V["NOT_SCION"])),
+                           (hfv.BR_NO_SCION_PATH, (2, V["NOT_IMPLEMENTED"])),
+                           (hfv.BR_NO_IPV4 if v6 else hfv.BR_NO_IPV6, (4, V["SCION_FORWARD"]))):
+            buf, lens = T.to_slots([frame])
+            a, v, e, s = orc.br_process(buf, lens, np.array([ifi], dtype=np.uint32), cfg, orc.hop_key(T.KEYS[1]),
+                                        feat_off=feat)
+            assert (int(a[0]), int(v[0])) == want, (v6, feat)
+            if want[0] == 2:
+                assert buf[0, :len(frame)].tobytes() == frame and int(e[0]) == -1
+        other = hfv.BR_NO_IPV6 if v6 else hfv.BR_NO_IPV4
+        with pytest.raises(hfv.HfvError, match="IPv%d support is deactivated" % (6 if v6 else 4)):
+            hfv.br_config_check_options(cfg, other)
+        hfv.br_config_check_options(cfg, hfv.BR_NO_SCION_PATH | (hfv.BR_NO_IPV4 if v6 else hfv.BR_NO_IPV6))
+
+
 def test_unknown_egress_aborts_and_falls_through():
     """VERDICT_ABORT is XDP_ABORTED = 0, not > 0: the MAC check and the redirect still run and
     record a second verdict (xdp.c:194, 256-283)."""

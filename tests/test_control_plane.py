@@ -174,6 +174,13 @@ def test_cli_attach_detach(pin_dir, tmp_path):
     assert bad.returncode != 0 and "Invalid argument" in bad.stderr
     bad = run("attach", str(tmp_path / "missing.toml"), env=env)
     assert bad.returncode != 0 and "Parsing configuration failed" in bad.stderr
+    # an IPv4 configuration on a router built without IPv4 (br-loader: STORE_IPV4 throws,
+    # maps.cpp:71-72, main prints "ERROR: ...", br_loader.cpp:291-294)
+    bad = run("attach", str(conf), "--no-ipv4", env=env)
+    assert bad.returncode != 0
+    assert "ERROR: Border router configuration contains IPv4 address, but IPv4 support is deactivated." in bad.stderr
+    r = run("attach", str(conf), "--no-ipv6", "--no-scion-path", env=env)
+    assert r.returncode == 0, r.stderr
     assert run("detach", "br1-x", env=env).returncode == 0
     # the file stays (an attached data plane keeps its mapping of this inode) and
     # carries the detached state; reading it reports "not attached"

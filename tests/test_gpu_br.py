@@ -30,12 +30,12 @@ def test_ptf_scenarios_gpu(gpu_ctx, v6):
         assert s[ifi, 0, 1] == len(frame) and s[ifi, 1, 1] == 1 and s.sum() == len(frame) + 1
 
 
-def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0, hf_check=True):
+def _compare(gpu_ctx, frames, lens, ifidx, cfg, key0, hf_check=True, feat_off=0):
     ref = frames.copy()
     oa, ov, oe, os_ = orc.br_process(ref, lens, ifidx, cfg, orc.hop_key(key0) if key0 is not None else None,
-                                     hf_check=hf_check)
+                                     hf_check=hf_check, feat_off=feat_off)
     got = frames.copy()
-    ga, gv, ge, gs = T.GpuBR(gpu_ctx, cfg, key0=key0, hf_check=hf_check).process(got, lens, ifidx)
+    ga, gv, ge, gs = T.GpuBR(gpu_ctx, cfg, key0=key0, hf_check=hf_check, feat_off=feat_off).process(got, lens, ifidx)
     bad = np.nonzero((ga != oa) | (gv != ov) | (ge != oe) | (got != ref).any(axis=1))[0]
     assert bad.size == 0, "first mismatch at frame %d: gpu (%d,%d,%d) oracle (%d,%d,%d)" % (
         bad[0], ga[bad[0]], gv[bad[0]], ge[bad[0]], oa[bad[0]], ov[bad[0]], oe[bad[0]])
@@ -106,6 +106,31 @@ def test_fuzz_parity_hf_check_off(gpu_ctx, v6):
     assert hfv.VERDICT["INVALID_HF"] not in v
     _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", v6), None, hf_check=False)   # no key: still forwarded
     gpu_ctx.br_set_hf_check(True)
+
+
+@pytest.mark.parametrize("opt", ["no_ipv6", "no_ipv4", "no_scion_path"])
+def test_fuzz_parity_build_options(gpu_ctx, opt):
+    """The reference's ENABLE_IPV4 / ENABLE_IPV6 / ENABLE_SCION_PATH builds (br/CMakeLists.txt:5-7):
+    an IPv4-only (IPv6-only) router over a mix of IPv4 and IPv6 frames passes the other family
+    up the stack as NOT_SCION; without the SCION path type every SCION frame is NOT_IMPLEMENTED.
+    Bit-exact against the oracle built the same way."""
+    v6cfg = opt == "no_ipv4"
+    mix = []
+    for v6 in (False, True):
+        brs = {b: T.OracleBR(T.br_config(b, v6)) for b in ("br1", "br2", "br3")}
+        mix.append(F.fuzz_batch(F.hop_inputs(brs, v6, MAC), "br1", v6, 4000, seed=300 + v6))
+    frames = np.concatenate([mix[0][0], mix[1][0]])
+    lens = np.concatenate([mix[0][1], mix[1][1]])
+    ifidx = np.concatenate([mix[0][2], mix[1][2]])
+    order = np.random.default_rng(5).permutation(len(frames))
+    frames, lens, ifidx = np.ascontiguousarray(frames[order]), lens[order], ifidx[order]
+    feat = {"no_ipv6": hfv.BR_NO_IPV6, "no_ipv4": hfv.BR_NO_IPV4, "no_scion_path": hfv.BR_NO_SCION_PATH}[opt]
+    v = _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1", v6cfg), T.KEYS[1], feat_off=feat)
+    if opt == "no_scion_path":
+        assert hfv.VERDICT["SCION_FORWARD"] not in v and hfv.VERDICT["NOT_IMPLEMENTED"] in v
+    else:
+        assert hfv.VERDICT["SCION_FORWARD"] in v and hfv.VERDICT["NOT_SCION"] in v
+    gpu_ctx.br_set_build_options(0)
 
 
 def test_large_batch_mixed_sizes(gpu_ctx):

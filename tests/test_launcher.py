@@ -23,7 +23,7 @@ def _bench(*args, timeout=300):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_dry_run_launches_n_ranks(n):
     d = _bench("--dry-run", "--gpus", str(n), "--n", "100", "--steps", "3", "--warmup", "1")
     assert d["n_gpus"] == n
@@ -39,9 +39,23 @@ def test_dry_run_single_rank_does_not_spawn():
 @pytest.mark.gpu
 def test_two_product_ranks_on_one_gpu():
     """Two ranks, each verifying its own resident records with the HIP kernels (launch path),
-    every bitmap checked against the generator truth inside bench.py."""
-    d = _bench("--gpus", "2", "--same-device", "--n", "65536", "--rotate", "2", "--steps", "4", "--warmup", "2",
-               "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
-    assert d["n_gpus"] == 2
+    every bitmap checked against the generator truth inside bench.py.  The line reports the
+    one physical GPU and the two ranks separately."""
+    d = _bench("--gpus", "2", "--same-device", "--launch-only", "--n", "65536", "--rotate", "2", "--steps", "4",
+               "--warmup", "2", "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
+    assert d["n_gpus"] == 1 and d["ranks"] == 2 and d["same_device"]["ranks"] == 2
     assert len(d["per_rank_ms"]["all"]) == 2
     assert d["value"] > 0 and d["roofline"]["kernel"] == "k_verify_records"
+
+
+@pytest.mark.gpu
+def test_two_service_ranks_on_one_gpu():
+    """the service path with two ranks on GPU 0, each resident grid limited to
+    half the CUs (HFV_SVC_GRID = CUs / ranks), both timed together; every bitmap is checked
+    against the generator truth inside bench.py, and each rank reports its thread budget."""
+    d = _bench("--gpus", "2", "--same-device", "--n", "262144", "--rotate", "2", "--steps", "8", "--warmup", "2",
+               "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
+    assert d["n_gpus"] == 1 and d["ranks"] == 2 and len(d["per_rank_ms"]["all"]) == 2
+    assert d["roofline"]["kernel"] == "k_verify_service" and d["value"] > 0
+    assert int(d["same_device"]["service_grid_blocks"]) * 2 <= 256
+    assert d["host_threads"]["ranks_on_node"] == 2 and d["host_threads"]["budget"] >= 2

@@ -334,6 +334,67 @@ __device__ __forceinline__ void fill_valid(const DevKeyTable *tab)
     if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
 }
 
+// ---------------------------------------------------------------------------------------
+// Per-interface keys with the round keys of rounds 3..10 expanded per packet (SchedKey).
+// LDS holds only three 16-byte rows per slot -- row 0 (rk0 ^ K1), row 11 (round 1 folded),
+// rk2 -- 12 KiB beside all four round tables, instead of the 48 KiB image beside two: the
+// random-slot ds_read_b128 of a key row costs ~3 conflict cycles per lane group (16 lanes over
+// 16 quad-banks), the four S-box lookups that derive the next round key (aes.c:120-137's
+// schedule step) are conflict-free T-table reads (32 lane copies).  11 -> 3 random rows and no
+// 16-bit rotation per column (the 4-table layout) for 32 extra conflict-free lookups per packet.
+static __shared__ uint4 s_keys3[3 * HFV_MAX_KEYS];
+
+__device__ __forceinline__ void fill_keys3(const DevKeyTable *tab, uint32_t nthr)
+{
+    // image rows 0 and 11 as stored; rk2 (image row 2, stored rotated by 16) unrotated
+    for (uint32_t e = threadIdx.x; e < 3 * HFV_MAX_KEYS; e += nthr) {
+        const uint32_t j = e / HFV_MAX_KEYS, k = e % HFV_MAX_KEYS;
+        const uint32_t *p = tab->rows[j == 0 ? 0 : j == 1 ? 11 : 2][k];
+        uint4 v = make_uint4(p[0], p[1], p[2], p[3]);
+        if (j == 2) v = make_uint4(rot16(v.x), rot16(v.y), rot16(v.z), rot16(v.w));
+        s_keys3[e] = v;
+    }
+    if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
+}
+
+// One AES-128 key-schedule step (FIPS-197 5.2; aes.c aes_key_expansion) on the 4-table LDS
+// layout: SubWord(RotWord(w3)) from four T-table reads whose S(x) byte already sits in the
+// output position -- T2[b1] byte 0, T0[b2] byte 1, T1[b3] byte 2, T2[b0] byte 3 -- merged by
+// two v_perm (disjoint bytes, so the xor below joins them).
+__device__ __forceinline__ uint4 next_round_key(const uint4 &rk, uint32_t rcon, const Lane &l)
+{
+    const uint32_t a = tlu<4, 1>(rk.w, l.b2, l), b = tlu<4, 2>(rk.w, l.b0, l);
+    const uint32_t c = tlu<4, 3>(rk.w, l.b1, l), d = tlu<4, 0>(rk.w, l.b2, l);
+    const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0500u);   // S(b1) | S(b2) << 8
+    const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x07020c0cu);   // S(b3) << 16 | S(b0) << 24
+    uint4 n;
+    n.x = xor3(rk.x, lo, hi) ^ rcon;
+    n.y = rk.y ^ n.x;
+    n.z = rk.z ^ n.y;
+    n.w = rk.w ^ n.z;
+    return n;
+}
+
+// Tag words 0..1 of a record-derived macinput for the slot's key (s_keys3 + expansion).
+__device__ __forceinline__ void cmac48_sched(const uint32_t w[4], uint32_t slot, const Lane &l, uint32_t &t0,
+                                             uint32_t &t1)
+{
+    const uint4 k0 = s_keys3[slot];
+    uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
+    round1_macinput<4>(s, s_keys3[HFV_MAX_KEYS + slot], l);
+    uint4 rk = s_keys3[2 * HFV_MAX_KEYS + slot];   // rk2
+    round_full<4>(s, rk, l);
+    uint32_t rcon = 0x04u;                         // round 3's (rcon_r = x^(r-1) in GF(2^8))
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+        rk = next_round_key(rk, rcon, l);
+        rcon = (rcon << 1) ^ ((rcon & 0x80u) ? 0x11bu : 0u);
+        round_full<4>(s, rk, l);
+    }
+    rk = next_round_key(rk, rcon, l);              // rk10, rcon 0x36
+    round_last_48<4>(s, rk, l, t0, t1);
+}
+
 // Tag words 0..1 for a record-derived macinput w[] (bytes 0,1,8,14,15 zero).
 template <int TAB, class K>
 __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &key, const Lane &l, uint32_t &t0,

@@ -186,6 +186,8 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
 // key-selection value for the kernels' template argument (the host still says
 // HFV_KEYSEL_IFID; the slot rule is the same, xdp.c:151-157).
 constexpr int kKeyselGather = 2;
+// ... or with three LDS rows per slot and rounds 3..10's keys expanded per packet (SchedKey).
+constexpr int kKeyselSched = 3;
 
 // One tile with the per-lane key rows already issued (GatherKey::issue): the verdict ballot.
 template <int TAB>
@@ -197,6 +199,19 @@ __device__ __forceinline__ uint64_t verify_tile_gather(const RecWords &r, uint64
     uint32_t t0, t1;
     cmac48_macinput<TAB>(w, key, l, t0, t1);
     const bool pass = t * 64 + lane < n && key.ok() && rec_tag_matches(r, t0, t1);
+    return __ballot(pass);
+}
+
+__device__ __forceinline__ uint64_t verify_tile_sched(const RecWords &r, uint64_t t, uint64_t n, uint32_t lane,
+                                                      const Lane &l)
+{
+    uint32_t w[4];
+    rec_macinput(r, w);
+    const uint32_t slot = rec_key_slot(r);
+    uint32_t t0, t1;
+    cmac48_sched(w, slot, l, t0, t1);
+    const bool ok = (s_valid[slot >> 5] >> (slot & 31)) & 1u;
+    const bool pass = t * 64 + lane < n && ok && rec_tag_matches(r, t0, t1);
     return __ballot(pass);
 }
 
@@ -985,6 +1000,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if (!relay) fill_keys(tab, nthr);
     } else if constexpr (KEYSEL == kKeyselGather) {
         fill_valid(tab);
+    } else if constexpr (KEYSEL == kKeyselSched) {
+        if (!relay) fill_keys3(tab, nthr);
     }
     __syncthreads();
     if (relay) {   // no barrier follows: the block's other waves go on without it
@@ -1079,6 +1096,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
         if constexpr (KEYSEL == kKeyselGather) {
             ballot = verify_tile_gather<TAB>(rc, cur.tile, cur.n, lane, l, gk);
+        } else if constexpr (KEYSEL == kKeyselSched) {
+            ballot = verify_tile_sched(rc, cur.tile, cur.n, lane, l);
         } else if (keyok) {
             RecWords c1[1] = {rc};
             verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
@@ -1152,12 +1171,19 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
                           uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid_out)
 {
-    // per-interface keys: key rows gathered into VGPRs beside the 4 LDS round tables (default),
-    // or HFV_SVC_IFID_LDS=1 for the round-2 layout (key image in LDS, 2 tables + rotation)
-    static const bool ifid_lds = getenv("HFV_SVC_IFID_LDS") && atoi(getenv("HFV_SVC_IFID_LDS"));
+    // Per-interface keys (config 3).  Default: three LDS rows per slot beside all four round
+    // tables, rounds 3..10's keys expanded per packet (SchedKey): bank-conflict cycles 1.37 M ->
+    // 0.38 M per 2^20 batch, LDS-active cycles -6 %, 0.5-2.6 % faster (profiles/r03/pmc/,
+    // ifid_ab/).  HFV_SVC_IFID=lds: the round-2 layout (48 KiB key image beside two tables and
+    // a 16-bit rotation per column).  HFV_SVC_IFID=gather: each packet's key rows gathered from
+    // L2 into VGPRs beside all four tables -- 2x slower (31 vs 63 Gpkt/s, profiles/r03/ifid_gather/):
+    // 11 scattered 16-byte loads per lane per tile hold the vector-memory path ~100 cycles each.
+    static const char *iv = getenv("HFV_SVC_IFID");
+    static const int ifv = !iv ? 2 : !strcmp(iv, "gather") ? 1 : !strcmp(iv, "lds") ? 0 : 2;
     auto k = keysel != HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_ZERO, 4>
-             : ifid_lds               ? k_verify_service<HFV_KEYSEL_IFID, 2>
-                                      : k_verify_service<kKeyselGather, 4>;
+             : ifv == 1               ? k_verify_service<kKeyselGather, 4>
+             : ifv == 2               ? k_verify_service<kKeyselSched, 4>
+                                      : k_verify_service<HFV_KEYSEL_IFID, 2>;
     const char *ge = getenv("HFV_SVC_GRID");   // experiments only: fewer blocks than CUs
     unsigned grid = ge && atoi(ge) > 0 && atoi(ge) < g.num_cus ? (unsigned)atoi(ge) : (unsigned)g.num_cus;
     if (grid > kSvcMaxBlocks) grid = kSvcMaxBlocks;

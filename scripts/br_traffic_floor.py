@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Config-4 traffic floor at the memory system's granularity, over bench.py's frame mix:
-reads in whole 128-byte L2 lines (gfx950) up to the last header byte the router reads, writes
-in 32-byte sectors holding a changed byte (from the oracle router's output), plus the 12 B of
-per-frame metadata.  Compare with bench.py's algorithmic bytes (exact bytes) and with PMC
-traffic (profiles/traffic.json br:1048576).  CPU only: python scripts/br_traffic_floor.py"""
+the 128-byte staged window of every frame (one L2 line: the kernel loads it whole), the header
+bytes read past the window in 32-byte sectors (the accessors load only those fields from HBM,
+so a second line is not fetched whole), writes in 32-byte sectors holding a changed byte (from
+the oracle router's output), plus the 12 B of per-frame metadata.  Compare with bench.py's
+algorithmic bytes (exact bytes) and with PMC traffic (profiles/traffic.json br:1048576).
+
+Round 2 counted the bytes past the window as a whole second 128-byte line; the PMC reads
+(157.4 B/frame) came in below that "floor" (160 B), which was therefore not one (VERDICT r02
+weak #3).  CPU only: python scripts/br_traffic_floor.py"""
 import json
 import os
 import sys
@@ -31,21 +36,26 @@ def main():
         changed = np.nonzero(slots[i] != before[i])[0]
         sectors = len(set((changed // 32).tolist()))
         hdr = abytes[i] - 12 - 35 - 2   # header bytes read (bench.py: hf_end + rewritten + metadata)
-        read_lines = -(-max(hdr, 128) // 128) * 128   # the staged 128-byte window at least
-        rows.append((abytes[i], read_lines + 32 * sectors + 12, read_lines, 32 * sectors))
+        past = max(0, hdr - 128)                       # header bytes read past the window
+        read_floor = 128 + 32 * -(-past // 32)
+        read_64 = 128 + 64 * -(-past // 64)            # the same at the 64-byte request size of a miss
+        rows.append((abytes[i], read_floor + 32 * sectors + 12, read_floor, 32 * sectors, read_64))
     # bench.br_batch draws template ids uniformly over the flows (half good, half corrupted MACs
     # at 1/16) -- weight every template pair equally, as the batch does
     a = np.array(rows, dtype=float)
     good = np.array(good)
     w = np.where(good, 15 / 16, 1 / 16)
     w = w / w.sum()
-    alg, floor, rd, wr = (float((a[:, j] * w).sum()) for j in range(4))
+    alg, floor, rd, wr, rd64 = (float((a[:, j] * w).sum()) for j in range(5))
     t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["br:1048576"]
     pmc = t["hbm_bytes_per_launch"] / 2**20
+    prd, pwr = t["read_bytes"] / 2**20, t["write_bytes"] / 2**20
     print(json.dumps({"algorithmic_bytes_per_frame": round(alg, 1), "granularity_floor_bytes_per_frame": round(floor, 1),
-                      "floor_read": round(rd, 1), "floor_write_sectors": round(wr, 1),
-                      "pmc_bytes_per_frame": round(pmc, 1), "pmc_over_algorithmic": round(pmc / alg, 3),
-                      "pmc_over_floor": round(pmc / floor, 3)}))
+                      "floor_read": round(rd + 6, 1), "floor_write": round(wr + 6, 1),
+                      "read_at_64B_requests": round(rd64 + 6, 1),
+                      "pmc_bytes_per_frame": round(pmc, 1), "pmc_read": round(prd, 1), "pmc_write": round(pwr, 1),
+                      "pmc_over_algorithmic": round(pmc / alg, 3), "pmc_over_floor": round(pmc / floor, 3),
+                      "pmc_read_over_floor": round(prd / (rd + 6), 3), "pmc_write_over_floor": round(pwr / (wr + 6), 3)}))
 
 
 if __name__ == "__main__":

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HFV_ABI_VERSION 1
+#define HFV_ABI_VERSION 2
 #define HFV_MAX_KEYS 256          /* key slots; the reference map holds 8 (maps.h:60-67) */
 #define HFV_REC_INF_OFF 40        /* default 64 B record layout, DESIGN.md section 3 */
 #define HFV_REC_HF_OFF 48
@@ -440,6 +440,16 @@ struct hfv_loop_config {
                                     2: copied to HBM by DMA, the kernel writes the bytes it changes
                                        and its outputs straight back into the ring */
     uint64_t *stats;             /* nullable: per-ifindex verdict counters (added to), as hfv_br_process_host */
+    /* Packet-socket I/O, the evaluation's veth loop (br/evaluation/veth_setup.bash,
+     * README.md:131-139) -- NULL: the in-process frame list above.
+     * rx_ifname: producers receive the frames tcpreplay pushes into the peer from an AF_PACKET
+     *            socket on this interface (frames/lens/n_frames unused); `total` bounds them,
+     *            and after idle_ms (0: 1000) without a frame the loop drains and returns.
+     * tx_ifname: consumers send every redirected frame out of an AF_PACKET socket on this
+     *            interface (count_and_drop.py counts them on the peer).
+     * Needs CAP_NET_RAW; -EPERM (or the socket's errno) otherwise. */
+    const char *rx_ifname, *tx_ifname;
+    int idle_ms;
 };
 struct hfv_loop_stats {
     uint64_t rx_pkts, tx_pkts, tx_bytes, drop_pkts;
@@ -448,6 +458,8 @@ struct hfv_loop_stats {
     double seconds;                             /* wall time of the whole loop */
     double gpu_busy_s, gpu_wait_s;              /* router stage: inside hfv_br_process_host / waiting for RX */
     double producer_busy_s, consumer_busy_s;    /* summed over the threads of each side */
+    uint64_t rx_truncated, tx_errors;           /* packet I/O: frames longer than a slot (dropped),
+                                                   sends that failed after retries */
 };
 int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *cfg, struct hfv_loop_stats *out);
 

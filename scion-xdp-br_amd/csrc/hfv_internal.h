@@ -204,6 +204,11 @@ uint32_t keymap_snapshot(const void *mapping, hop_key *slots, uint32_t valid[8])
 // array dstats (nullable).  dout (nullable: in place) receives the changed bytes of each frame
 // and must already hold the rest of it (the host ring a DMA copy came from).
 int br_zc_prepare(hfv_ctx *ctx);
+// Test-only host router stage for hfv_loop_run (hfv_debug_loop_host_stage, not in the public
+// header): frames of one chunk in place, outputs as the kernel writes them; 0 = ok.
+typedef int (*hfv_loop_host_stage_fn)(void *user, uint8_t *frames, size_t slot, const uint16_t *len,
+                                      const uint32_t *ingress_ifindex, size_t n, uint8_t *action, uint8_t *verdict,
+                                      int32_t *egress_ifindex);
 int br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot, const uint16_t *dlen, const uint32_t *difx,
                   size_t n, uint8_t *dact, uint8_t *dver, int32_t *degr, uint64_t *dstats, uint8_t *dout = nullptr);
 // Before destroying a stream that launched with the ctx's tables (after synchronizing it):

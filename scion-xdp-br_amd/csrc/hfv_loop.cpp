@@ -10,12 +10,19 @@
 // free (a consumer read the verdicts and the transmitted frames), each stage on its own
 // threads, so producer, GPU and consumer work on different chunks at once.  Producer and
 // consumer threads run on the CPUs of the GPU's NUMA node.
+#include <arpa/inet.h>
 #include <errno.h>
+#include <linux/if_packet.h>
+#include <net/ethernet.h>
+#include <net/if.h>
+#include <poll.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <thread>
@@ -90,6 +97,45 @@ static void pin(int numa_node)
     if (CPU_COUNT(&cpus) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus, &cpus);
 }
 
+// ---- packet sockets (the evaluation's veth ends) ---------------------------------------------
+// One AF_PACKET socket per side, bound to its interface: RX shared by the producer threads
+// (recvmmsg straight into ring slots), TX shared by the consumers (sendmmsg from ring slots).
+static int packet_socket(const char *ifname, bool rx, int *out)
+{
+    const unsigned idx = if_nametoindex(ifname);
+    if (!idx) return -ENODEV;
+    const int fd = socket(AF_PACKET, SOCK_RAW, rx ? htons(ETH_P_ALL) : 0);
+    if (fd < 0) return -errno;
+    struct sockaddr_ll a;
+    memset(&a, 0, sizeof a);
+    a.sll_family = AF_PACKET;
+    a.sll_protocol = rx ? htons(ETH_P_ALL) : 0;
+    a.sll_ifindex = (int)idx;
+    if (bind(fd, (struct sockaddr *)&a, sizeof a) != 0) {
+        const int e = -errno;
+        close(fd);
+        return e;
+    }
+    if (rx) {
+#ifdef PACKET_IGNORE_OUTGOING
+        int one = 1;   // only frames arriving on the interface, not ones sent from it
+        (void)setsockopt(fd, SOL_PACKET, PACKET_IGNORE_OUTGOING, &one, sizeof one);
+#endif
+        int buf = 64 << 20;   // a burst of a few hundred thousand frames
+        if (setsockopt(fd, SOL_SOCKET, SO_RCVBUFFORCE, &buf, sizeof buf) != 0)
+            (void)setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+    }
+    *out = fd;
+    return 0;
+}
+
+static double mono_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
 // Ring slot of chunk k: state = 3k (free for chunk k), 3k + 1 (filled), 3k + 2 (processed); the
 // consumer of chunk k hands the slot to chunk k + chunks.  Tagging the state with the chunk
 // number keeps two producers (or consumers) whose chunks share a slot from both taking it.
@@ -98,35 +144,79 @@ struct Chunk {
     size_t n = 0;                     // frames in it
 };
 
+// Test-only router stage on the host (hfv_debug_loop_host_stage): with it set, hfv_loop_run
+// takes no ctx, keeps the ring in ordinary memory and calls the function on each filled chunk
+// in place of the kernel, so the ring, the threads and the packet-socket I/O run on a machine
+// without a GPU (tests/test_loop_pktio.py drives them over veth pairs with the oracle router).
+static hfv::hfv_loop_host_stage_fn g_host_stage = nullptr;
+static void *g_host_stage_user = nullptr;
+
 }  // namespace
 
 using namespace hfv;
 
+extern "C" int hfv_debug_loop_host_stage(hfv::hfv_loop_host_stage_fn fn, void *user)
+{
+    g_host_stage = fn;
+    g_host_stage_user = user;
+    return 0;
+}
+
 extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struct hfv_loop_stats *out)
 {
-    if (!ctx || !c || !out || !c->frames || !c->lens || c->n_frames == 0) return fail(-EINVAL, "null argument");
+    const hfv::hfv_loop_host_stage_fn host_stage = g_host_stage;
+    void *const host_user = g_host_stage_user;
+    const bool pkt_rx = c && c->rx_ifname, pkt_tx = c && c->tx_ifname;
+    if ((!ctx && !host_stage) || !c || !out || (!pkt_rx && (!c->frames || !c->lens || c->n_frames == 0)))
+        return fail(-EINVAL, "null argument");
     if (c->slot < 128 || (c->slot & 15) || c->chunk == 0 || c->chunks < 2 || c->total == 0 || c->dma < 0 || c->dma > 2)
         return fail(-EINVAL, "slot must be a multiple of 16 and >= 128, chunk > 0, chunks >= 2, total > 0, dma 0..2");
-    for (size_t i = 0; i < c->n_frames; ++i)
+    for (size_t i = 0; !pkt_rx && i < c->n_frames; ++i)
         if (c->lens[i] > c->slot || c->lens[i] > c->frame_stride) return fail(-EINVAL, "frame %zu longer than its slot", i);
     memset(out, 0, sizeof *out);
     const size_t nslots = c->chunk * c->chunks;
     const int producers = c->producers > 0 ? c->producers : 1, consumers = c->consumers > 0 ? c->consumers : 1;
+    int rx_fd = -1, tx_fd = -1, rc = 0;
+    if (pkt_rx && (rc = packet_socket(c->rx_ifname, true, &rx_fd)) != 0)
+        return fail(rc, "loop: AF_PACKET socket on %s: %s", c->rx_ifname, strerror(-rc));
+    if (pkt_tx && (rc = packet_socket(c->tx_ifname, false, &tx_fd)) != 0) {
+        if (rx_fd >= 0) close(rx_fd);
+        return fail(rc, "loop: AF_PACKET socket on %s: %s", c->tx_ifname, strerror(-rc));
+    }
+    auto close_sockets = [&]() {
+        if (rx_fd >= 0) close(rx_fd);
+        if (tx_fd >= 0) close(tx_fd);
+    };
     // the RX ring and the per-frame metadata in pinned, mapped host memory: the kernel reads
     // and writes them in place (zero-copy), or the DMA engines copy them (dma = 1: both ways;
     // dma = 2: in only, the kernel writing its changes back into the ring)
-    int rc = br_zc_prepare(ctx);   // stops a running service; the ctx's device is current
-    if (rc) return rc;
     const size_t ring_bytes = (nslots * c->slot + 4095) & ~(size_t)4095;
     const size_t meta_bytes = (nslots * 16 + 4095) & ~(size_t)4095;
     uint8_t *ring = nullptr, *meta = nullptr, *dring = nullptr, *dmeta = nullptr;
-    if (hipHostMalloc((void **)&ring, ring_bytes, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc((void **)&meta, meta_bytes, hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&dring, ring, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&dmeta, meta, 0) != hipSuccess) {
-        if (ring) (void)hipHostFree(ring);
-        if (meta) (void)hipHostFree(meta);
-        return fail(-ENOMEM, "loop: pinned ring allocation");
+    if (host_stage) {
+        ring = (uint8_t *)aligned_alloc(4096, ring_bytes);
+        meta = (uint8_t *)aligned_alloc(4096, meta_bytes);
+        if (!ring || !meta) {
+            free(ring);
+            free(meta);
+            close_sockets();
+            return fail(-ENOMEM, "loop: ring allocation");
+        }
+    } else {
+        rc = br_zc_prepare(ctx);   // stops a running service; the ctx's device is current
+        if (rc) {
+            close_sockets();
+            return rc;
+        }
+        if (hipHostMalloc((void **)&ring, ring_bytes, hipHostMallocMapped) != hipSuccess ||
+            hipHostMalloc((void **)&meta, meta_bytes, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&dring, ring, 0) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&dmeta, meta, 0) != hipSuccess) {
+            if (ring) (void)hipHostFree(ring);
+            if (meta) (void)hipHostFree(meta);
+            close_sockets();
+            return fail(-ENOMEM, "loop: pinned ring allocation");
+        }
     }
     memset(meta, 0, meta_bytes);
     // per-frame metadata, chunk by chunk: len u16 (in a 4 B/frame field) | ingress ifindex u32 |
@@ -137,11 +227,88 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     auto egr_of = [&](size_t s) { return (int32_t *)(meta + s * C * 16 + C * 8); };
     auto act_of = [&](size_t s) { return meta + s * C * 16 + C * 12; };
     auto ver_of = [&](size_t s) { return meta + s * C * 16 + C * 13; };
-    const int node = hfv_ctx_numa_node(ctx);
+    const int node = ctx ? hfv_ctx_numa_node(ctx) : -1;
     std::vector<Chunk> ch(c->chunks);
     for (size_t i = 0; i < c->chunks; ++i) ch[i].state.store(3 * i);
     const uint64_t nchunks_total = (c->total + c->chunk - 1) / c->chunk;
     std::atomic<bool> abort{false};
+    // packet RX: the time of the last frame received (or of the start) and the end of input
+    const double idle_s = (c->idle_ms > 0 ? c->idle_ms : 1000) * 1e-3;
+    std::atomic<double> last_rx{mono_s()};
+    std::atomic<bool> rx_done{false};
+    std::atomic<uint64_t> rx_trunc{0}, tx_err{0};
+    // Fill up to n slots from the RX socket; returns the frames received (fewer once the input
+    // has been idle for idle_s, which ends the input for every producer).
+    auto receive = [&](size_t base, size_t n, uint16_t *len, uint32_t *ifx) -> size_t {
+        constexpr size_t kBatch = 64;
+        struct mmsghdr mm[kBatch];
+        struct iovec iov[kBatch];
+        size_t got = 0;
+        while (got < n && !rx_done.load(std::memory_order_relaxed) && !abort.load(std::memory_order_relaxed)) {
+            struct pollfd pf = {rx_fd, POLLIN, 0};
+            if (poll(&pf, 1, 5) <= 0) {
+                if (mono_s() - last_rx.load(std::memory_order_relaxed) > idle_s) rx_done.store(true);
+                continue;
+            }
+            const size_t want = n - got < kBatch ? n - got : kBatch;
+            for (size_t j = 0; j < want; ++j) {
+                iov[j].iov_base = ring + (base + got + j) * c->slot;
+                iov[j].iov_len = c->slot;
+                memset(&mm[j], 0, sizeof mm[j]);
+                mm[j].msg_hdr.msg_iov = &iov[j];
+                mm[j].msg_hdr.msg_iovlen = 1;
+            }
+            const int r = recvmmsg(rx_fd, mm, (unsigned)want, MSG_DONTWAIT | MSG_TRUNC, nullptr);
+            if (r <= 0) continue;
+            last_rx.store(mono_s(), std::memory_order_relaxed);
+            // keep the frames that fit a slot, packed in arrival order
+            size_t kept = 0;
+            for (int j = 0; j < r; ++j) {
+                const size_t l = mm[j].msg_len;
+                if (l > c->slot || (mm[j].msg_hdr.msg_flags & MSG_TRUNC)) {
+                    rx_trunc.fetch_add(1);
+                    continue;
+                }
+                if (kept != (size_t)j) memmove(ring + (base + got + kept) * c->slot, ring + (base + got + j) * c->slot, l);
+                len[got + kept] = (uint16_t)l;
+                ifx[got + kept] = c->rx_ifindex;
+                ++kept;
+            }
+            got += kept;
+        }
+        return got;
+    };
+    // Send the redirected frames of a chunk out of the TX socket, in batches.
+    auto transmit = [&](size_t base, size_t n, const uint16_t *len, const uint8_t *act) {
+        constexpr size_t kBatch = 64;
+        struct mmsghdr mm[kBatch];
+        struct iovec iov[kBatch];
+        size_t m = 0;
+        auto flush = [&]() {
+            size_t sent = 0;
+            for (int tries = 0; sent < m && tries < 64; ++tries) {
+                const int r = sendmmsg(tx_fd, mm + sent, (unsigned)(m - sent), 0);
+                if (r > 0) {
+                    sent += (size_t)r;
+                } else {
+                    struct timespec ts = {0, 20000};   // ENOBUFS: the device queue is full
+                    nanosleep(&ts, nullptr);
+                }
+            }
+            if (sent < m) tx_err.fetch_add(m - sent);
+            m = 0;
+        };
+        for (size_t i = 0; i < n; ++i) {
+            if (act[i] != 4) continue;
+            iov[m].iov_base = ring + (base + i) * c->slot;
+            iov[m].iov_len = len[i];
+            memset(&mm[m], 0, sizeof mm[m]);
+            mm[m].msg_hdr.msg_iov = &iov[m];
+            mm[m].msg_hdr.msg_iovlen = 1;
+            if (++m == kBatch) flush();
+        }
+        if (m) flush();
+    };
 
     // producers: chunk k by producer k % P (tcpreplay --loop of the frame list)
     std::vector<double> busy(producers, 0.0);
@@ -156,12 +323,16 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             uint16_t *len = len_of(sl);
             uint32_t *ifx = ifx_of(sl);
             const uint64_t first = k * C;
-            const size_t n = (size_t)(c->total - first < C ? c->total - first : C);
-            for (size_t i = 0; i < n; ++i) {
-                const size_t f = (size_t)((first + i) % c->n_frames);
-                memcpy(ring + (base + i) * c->slot, c->frames + f * c->frame_stride, c->lens[f]);
-                len[i] = c->lens[f];
-                ifx[i] = c->rx_ifindex;
+            size_t n = (size_t)(c->total - first < C ? c->total - first : C);
+            if (pkt_rx) {
+                n = receive(base, n, len, ifx);   // fewer (or none) once the input went idle
+            } else {
+                for (size_t i = 0; i < n; ++i) {
+                    const size_t f = (size_t)((first + i) % c->n_frames);
+                    memcpy(ring + (base + i) * c->slot, c->frames + f * c->frame_stride, c->lens[f]);
+                    len[i] = c->lens[f];
+                    ifx[i] = c->rx_ifindex;
+                }
             }
             cc.n = n;
             busy[p] += now_s() - tb;
@@ -194,6 +365,7 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
                     s.drop_pkts++;
                 }
             }
+            if (pkt_tx) transmit(base, cc.n, len, act);
             s.consumer_busy_s += now_s() - tb;
             cc.state.store(3 * (k + c->chunks), std::memory_order_release);
         }
@@ -211,7 +383,7 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     const bool split = c->dma == 2 && split_env;
     uint64_t *dstats = nullptr;
     const size_t stats_bytes = HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8;
-    for (int i = 0; i < D && !rc; ++i) {
+    for (int i = 0; i < D && !rc && !host_stage; ++i) {
         if (hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
             rc = fail(-EIO, "loop: stream/event creation failed");
@@ -221,10 +393,10 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
             rc = fail(-EIO, "loop: stream/event creation failed");
     }
     std::vector<uint8_t *> dfr(D, nullptr), dmt(D, nullptr);   // DMA variant: device twin per stream
-    for (int i = 0; i < D && !rc && c->dma; ++i)
+    for (int i = 0; i < D && !rc && c->dma && !host_stage; ++i)
         if (hipMalloc((void **)&dfr[i], C * c->slot) != hipSuccess || hipMalloc((void **)&dmt[i], C * 16) != hipSuccess)
             rc = fail(-ENOMEM, "loop: device chunk buffers");
-    if (!rc && c->stats && (hipMalloc((void **)&dstats, stats_bytes) != hipSuccess ||
+    if (!rc && c->stats && !host_stage && (hipMalloc((void **)&dstats, stats_bytes) != hipSuccess ||
                             hipMemset(dstats, 0, stats_bytes) != hipSuccess))
         rc = fail(-ENOMEM, "loop: device counters");
     // streams, events and device buffers before the clock starts; the threads only when they are there
@@ -259,6 +431,24 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         const size_t sl = k % c->chunks;
         uint8_t *fr = ring + sl * C * c->slot, *cm = meta + sl * C * 16;
         const int q = (int)(k % D);
+        if (host_stage) {   // test-only host router stage: synchronous, in ring order
+            if (cc.n && host_stage(host_user, fr, c->slot, (const uint16_t *)cm, (const uint32_t *)(cm + C * 4), cc.n,
+                                   cm + C * 12, cm + C * 13, (int32_t *)(cm + C * 8)) != 0)
+                rc = fail(-EIO, "loop: host stage failed");
+            if (!rc) ch[sl].state.store(3 * k + 2, std::memory_order_release);
+            ++launched;
+            ++retired;
+            gpu_wait += tb - tw;
+            gpu_busy += now_s() - tb;
+            continue;
+        }
+        if (cc.n == 0) {   // packet input ended before this chunk: nothing to route
+            while (!rc && retired < launched) retire(true);
+            if (!rc) ch[sl].state.store(3 * k + 2, std::memory_order_release);
+            ++launched;
+            ++retired;
+            continue;
+        }
         if (!c->dma) {   // the kernel on the mapped ring (device addresses of the same pages)
             uint8_t *dfr_zc = dring + sl * C * c->slot, *dm = dmeta + sl * C * 16;
             rc = br_dev_launch(ctx, ss[q], dfr_zc, c->slot, (uint16_t *)dm, (uint32_t *)(dm + C * 4), cc.n, dm + C * 12,
@@ -305,6 +495,9 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     }
     if (rc) abort.store(true);
     for (auto &t : th) t.join();
+    out->rx_truncated = rx_trunc.load();
+    out->tx_errors = tx_err.load();
+    close_sockets();
     const double t1 = now_s();
     out->seconds = t1 - t0;
     out->gpu_busy_s = gpu_busy;
@@ -337,7 +530,12 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
         if (dfr[i]) (void)hipFree(dfr[i]);
         if (dmt[i]) (void)hipFree(dmt[i]);
     }
-    (void)hipHostFree(ring);
-    (void)hipHostFree(meta);
+    if (host_stage) {
+        free(ring);
+        free(meta);
+    } else {
+        (void)hipHostFree(ring);
+        (void)hipHostFree(meta);
+    }
     return rc;
 }

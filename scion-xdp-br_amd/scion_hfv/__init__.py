@@ -227,7 +227,8 @@ class LoopConfig(ctypes.Structure):
                 ("frame_stride", ctypes.c_size_t), ("rx_ifindex", ctypes.c_uint32), ("slot", ctypes.c_uint32),
                 ("chunk", ctypes.c_size_t), ("chunks", ctypes.c_size_t), ("total", ctypes.c_uint64),
                 ("producers", ctypes.c_int), ("consumers", ctypes.c_int), ("digest", ctypes.c_int),
-                ("inflight", ctypes.c_int), ("dma", ctypes.c_int), ("stats", ctypes.c_void_p)]
+                ("inflight", ctypes.c_int), ("dma", ctypes.c_int), ("stats", ctypes.c_void_p),
+                ("rx_ifname", ctypes.c_char_p), ("tx_ifname", ctypes.c_char_p), ("idle_ms", ctypes.c_int)]
 
 
 class LoopStats(ctypes.Structure):
@@ -236,7 +237,45 @@ class LoopStats(ctypes.Structure):
                 ("drop_pkts", ctypes.c_uint64), ("tx_digest", ctypes.c_uint64),
                 ("verdict_pkts", ctypes.c_uint64 * 11), ("seconds", ctypes.c_double),
                 ("gpu_busy_s", ctypes.c_double), ("gpu_wait_s", ctypes.c_double),
-                ("producer_busy_s", ctypes.c_double), ("consumer_busy_s", ctypes.c_double)]
+                ("producer_busy_s", ctypes.c_double), ("consumer_busy_s", ctypes.c_double),
+                ("rx_truncated", ctypes.c_uint64), ("tx_errors", ctypes.c_uint64)]
+
+
+def loop_run(handle, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
+             consumers=2, digest=False, stats=None, inflight=2, dma=0, rx_ifname=None, tx_ifname=None, idle_ms=0):
+    """hfv_loop_run on ctx handle `handle` (None only with a host stage, debug_loop_host_stage)."""
+    import numpy as np
+    if frames is not None:
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    cfg = LoopConfig(frames=frames.ctypes.data if frames is not None else None,
+                     lens=lens.ctypes.data if lens is not None else None,
+                     n_frames=frames.shape[0] if frames is not None else 0,
+                     frame_stride=frames.shape[1] if frames is not None else 0, rx_ifindex=rx_ifindex, slot=slot,
+                     chunk=chunk, chunks=chunks, total=total, producers=producers, consumers=consumers,
+                     digest=1 if digest else 0, inflight=inflight, dma=int(dma), stats=_ptr(stats),
+                     rx_ifname=rx_ifname.encode() if rx_ifname else None,
+                     tx_ifname=tx_ifname.encode() if tx_ifname else None, idle_ms=idle_ms)
+    st = LoopStats()
+    _check(lib().hfv_loop_run(handle, ctypes.byref(cfg), ctypes.byref(st)))
+    return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,
+            "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds,
+            "gpu_busy_s": st.gpu_busy_s, "gpu_wait_s": st.gpu_wait_s, "producer_busy_s": st.producer_busy_s,
+            "consumer_busy_s": st.consumer_busy_s, "rx_truncated": st.rx_truncated, "tx_errors": st.tx_errors}
+
+
+# Test-only host router stage for hfv_loop_run (see hfv_loop.cpp): fn(frames, slot, len,
+# ingress_ifindex, n, action, verdict, egress) on raw pointers; keep the returned object alive.
+LOOP_HOST_STAGE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
+
+
+def debug_loop_host_stage(fn):
+    """Install fn (a LOOP_HOST_STAGE) as hfv_loop_run's router stage, None to remove it."""
+    L = lib()
+    L.hfv_debug_loop_host_stage.argtypes = [LOOP_HOST_STAGE, ctypes.c_void_p]
+    L.hfv_debug_loop_host_stage.restype = ctypes.c_int
+    _check(L.hfv_debug_loop_host_stage(fn if fn is not None else LOOP_HOST_STAGE(), None))
 
 
 def loop_frame_digest(frame: bytes, egress: int) -> int:
@@ -386,25 +425,13 @@ class Ctx:
         _check(lib().hfv_br_process_host(self._h, _ptr(frames), slot, _ptr(lens), _ptr(ingress_ifindex), n, window,
                                          _ptr(action), _ptr(verdict), _ptr(egress_ifindex), _ptr(stats)))
 
-    def loop_run(self, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
-                 consumers=2, digest=False, stats=None, inflight=2, dma=0):
+    def loop_run(self, frames, lens, total, **kw):
         """Config 5 in one process (hfv_loop_run): `frames` (n x stride uint8) cycled into a
         registered RX ring, the router over each chunk, TX/drop consumers.  dma: 0 zero-copy,
         1 (or True) copies both ways, 2 copies in and the kernel writes its changes back.
+        rx_ifname / tx_ifname: packet-socket I/O on those interfaces instead (frames unused).
         Returns a dict."""
-        import numpy as np
-        frames = np.ascontiguousarray(frames, dtype=np.uint8)
-        lens = np.ascontiguousarray(lens, dtype=np.uint16)
-        cfg = LoopConfig(frames=frames.ctypes.data, lens=lens.ctypes.data, n_frames=frames.shape[0],
-                         frame_stride=frames.shape[1], rx_ifindex=rx_ifindex, slot=slot, chunk=chunk,
-                         chunks=chunks, total=total, producers=producers, consumers=consumers,
-                         digest=1 if digest else 0, inflight=inflight, dma=int(dma), stats=_ptr(stats))
-        st = LoopStats()
-        _check(lib().hfv_loop_run(self._h, ctypes.byref(cfg), ctypes.byref(st)))
-        return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,
-                "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds,
-                "gpu_busy_s": st.gpu_busy_s, "gpu_wait_s": st.gpu_wait_s, "producer_busy_s": st.producer_busy_s,
-                "consumer_busy_s": st.consumer_busy_s}
+        return loop_run(self._h, frames, lens, total, **kw)
 
     @staticmethod
     def debug_publish_delay(us):

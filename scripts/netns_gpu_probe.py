@@ -4,8 +4,8 @@ creates the evaluation's veth pairs over rtnetlink, then touches the GPU from in
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-import netns  # noqa: E402  (scripts/netns.py: stdlib only; no GPU yet)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+import netns  # noqa: E402  (tests/netns.py: stdlib only; no GPU yet)
 
 print("uid", os.getuid(), "probe:", netns.probe(), flush=True)
 import socket  # noqa: E402

@@ -97,9 +97,16 @@ def set_mac(name, mac):
 
 def evaluation_links():
     """veth_setup.bash: veth0-veth1 and veth2-veth3 with the MACs 02:00:00:00:00:0N, up.
-    Returns {name: ifindex}."""
+    Returns {name: ifindex}.  IPv6 is switched off on them first, so the kernel's own neighbour
+    discovery frames do not join the test traffic."""
     for a, b in (("veth0", "veth1"), ("veth2", "veth3")):
         veth_pair(a, b)
+    for k in range(4):
+        try:
+            with open("/proc/sys/net/ipv6/conf/veth%d/disable_ipv6" % k, "w") as f:
+                f.write("1")
+        except OSError:
+            pass
     for k in range(4):
         set_mac("veth%d" % k, "02:00:00:00:00:%02x" % k)
         set_up("veth%d" % k)

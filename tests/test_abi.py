@@ -37,7 +37,7 @@ def test_lib_exports_every_declared_symbol():
     assert not missing, missing
     assert "AES_SBox" in exported
     L = hfv.lib()
-    assert L.hfv_abi_version() == 1
+    assert L.hfv_abi_version() == 2
 
 
 def test_exported_sbox():

@@ -127,7 +127,33 @@ def test_new_entry_points_reject_bad_arguments_without_gpu():
     assert L.hfv_service_run(None, None, 0, ctypes.byref(t), ctypes.byref(ms)) == -errno.EINVAL
     assert L.hfv_verdict_counters(None, None, 64, 1, None, None, None) == -errno.EINVAL
     assert "NULL" in L.hfv_last_error().decode() or "null" in L.hfv_last_error().decode()
-    assert ctypes.sizeof(hfv.LoopStats) == 8 * (5 + hfv.BR_COUNTERS) + 8 * 5
+    assert ctypes.sizeof(hfv.LoopStats) == 8 * (5 + hfv.BR_COUNTERS) + 8 * 5 + 8 * 2
+
+
+def test_ctypes_layouts_match_the_c_header(tmp_path):
+    """The ctypes mirrors of the public structs have the C header's size and field offsets
+    (compiled with gcc against include/scion_hfv.h)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    checks = {"hfv_loop_config": (hfv.LoopConfig, ["rx_ifindex", "total", "dma", "stats", "rx_ifname", "idle_ms"]),
+              "hfv_loop_stats": (hfv.LoopStats, ["verdict_pkts", "seconds", "rx_truncated", "tx_errors"]),
+              "hfv_br_config": (hfv.BrConfig, ["egress", "routes", "tx_ports"])}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "scion_hfv.h"', "int main(void) {"]
+    for st, (_, fields) in checks.items():
+        src.append('printf("%%zu\\n", sizeof(struct %s));' % st)
+        for f in fields:
+            src.append('printf("%%zu\\n", offsetof(struct %s, %s));' % (st, f))
+    src.append("return 0; }")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(root, "include"), str(c), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = []
+    for st, (cls, fields) in checks.items():
+        want.append(ctypes.sizeof(cls))
+        want += [getattr(cls, f).offset for f in fields]
+    assert got == want
 
 
 def test_loop_frame_digest_is_order_free():

@@ -142,10 +142,13 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path);
  * recs: n records of `stride` bytes (8-byte aligned, stride % 8 == 0). */
 int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                        void *stream);
-/* record_verdict (xdp.c:54-70) for the verify-only paths: counters[slot][0] += packets that
- * verified, counters[slot][1] += packets dropped as VERDICT_INVALID_HF, where slot is the
- * packet's AS-ingress interface (IFID & 0xff, Cons ? HF.ingress : HF.egress, xdp.c:151-157),
- * from the records and the verdict bitmap hfv_verify_records or the service wrote for them.
+/* Verdict counts for the verify-only paths, modelled on record_verdict (xdp.c:54-70) but NOT
+ * its layout: counters[slot][0] += packets that verified, counters[slot][1] += packets dropped
+ * as VERDICT_INVALID_HF, where slot is the packet's AS-ingress interface (IFID & 0xff,
+ * Cons ? HF.ingress : HF.egress, xdp.c:151-157) -- an IFID-keyed approximation with packet
+ * counts only; the reference's port_stats_map is keyed by the receiving ifindex and also counts
+ * bytes, so these do not compare with it (hfv_br_process's counters do).
+ * From the records and the verdict bitmap hfv_verify_records or the service wrote for them.
  * counters: device u64[256][2], added to.  Stream-ordered like hfv_verify_records. */
 int hfv_verdict_counters(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, const uint64_t *pass_bits,
                          uint64_t *counters, void *stream);

@@ -832,7 +832,7 @@ def run_hf(args, W):
     elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
     bytes_per_batch = BYTES_PER_PACKET * n
     if headline == "service":
-        achieved = bytes_per_batch * args.steps / (m["grid_ms"] * 1e-3) / 1e9
+        achieved = bytes_per_batch * args.steps / (max(m["grid_ms"], 1e-9) * 1e-3) / 1e9   # 0: HFV_SVC_NOEV
         kern = {"kernel": "k_verify_service", "grid_ms": round(m["grid_ms"], 4), "batches_per_grid": args.steps,
                 "kernel_ms_per_batch": round(m["grid_ms"] / args.steps, 5),
                 "algorithmic_bytes_per_batch": int(bytes_per_batch),

@@ -1542,6 +1542,14 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
     return 0;
 }
 
+// Diagnostics: HFV_SVC_NOEV=1 launches the service grid without the dispatch start/stop events
+// (its lifetime then reads 0 ms) -- to measure what the events cost a timed region.
+static bool svc_noev()
+{
+    static const bool v = getenv("HFV_SVC_NOEV") && atoi(getenv("HFV_SVC_NOEV"));
+    return v;
+}
+
 static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
 {
     if (kernel_ms) *kernel_ms = 0.0f;
@@ -1571,7 +1579,7 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     ctx->svc_running = false;
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;
-    if (kernel_ms) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
+    if (kernel_ms && !svc_noev()) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
     // A grid that left on the stop descriptor verified every batch before it (each block
     // reaches the stop only after its share of all earlier batches).  An idle or watchdog
     // exit is clean unless it left a posted batch unverified (batches may complete out of
@@ -1647,9 +1655,10 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
 
 static int svc_launch(hfv_ctx *ctx, DevState *ds)
 {
+    const bool noev = svc_noev();
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
                                   ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream,
-                                  ctx->svc_ev[0], ctx->svc_ev[1], &ctx->svc_grid);
+                                  noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ctx->svc_running = true;

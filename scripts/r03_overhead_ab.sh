@@ -7,9 +7,10 @@ OUT=gpurun_out/${1:-r03_overhead}
 mkdir -p $OUT
 ARGS="--steps 20 --warmup 5 --no-extras --no-host-e2e --cpu-budget 0 --loop-n 0 --svc-reps 5"
 for i in 1 2 3; do
-    for v in base devkernarg skipargcopy nodirect; do
+    for v in base noev devkernarg skipargcopy nodirect; do
         case $v in
             base) E="" ;;
+            noev) E="HFV_SVC_NOEV=1" ;;
             devkernarg) E="HIP_FORCE_DEV_KERNARG=1" ;;
             skipargcopy) E="ROC_SKIP_KERNEL_ARG_COPY=1" ;;
             nodirect) E="AMD_DIRECT_DISPATCH=0" ;;

@@ -382,25 +382,45 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
             svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
         svc["call_us"] = (time.perf_counter() - t) * 1e6
 
-    # the K-step timed region is repeated `reps` times (each a fresh grid over the same K
+    # The K-step timed region is repeated `reps` times (each a fresh grid over the same K
     # batches) and the median region is reported: one timed region of ~0.3 ms is exposed to a
-    # single host hiccup (one of three A/B runs measured 0.41 ms for a 0.245 ms grid)
-    runs = []
-    for _ in range(max(1, reps)):
-        for b in bitmaps:
-            b.zero_()
-        W.sync()
-        el, per_rank = W.timed(1, service_run)
-        if run_async:
-            svc["grid_ms"] = ctx.service_stop()   # reaps the exited grid: its lifetime
-        runs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"]))   # diagnostics
-        check(steps)
+    # single host hiccup (one of three A/B runs measured 0.41 ms for a 0.245 ms grid).
+    # `value` comes from regions whose grid carries no dispatch timing events: on MI355X the
+    # events add ~12 us to a launch-to-synchronize round trip (24.7 against 12.5 us for the
+    # same kernel, scripts/ubench/launch_cost.hip, profiles/r03/launch_cost/), i.e. ~4 % of a
+    # K = 20 region.  The grid lifetime the roofline needs is timed with the events in `reps`
+    # further regions that are identical otherwise (HFV_BENCH_TIMED_VALUE=1: value from those).
+    timed_value = os.environ.get("HFV_BENCH_TIMED_VALUE", "0") != "0"
+
+    def regions(timing):
+        ctx.service_set_timing(timing)
+        rs = []
+        for _ in range(max(1, reps)):
+            for b in bitmaps:
+                b.zero_()
+            W.sync()
+            el, per_rank = W.timed(1, service_run)
+            if run_async:
+                svc["grid_ms"] = ctx.service_stop()   # reaps the exited grid: its lifetime (0 untimed)
+            rs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"]))   # diagnostics
+            check(steps)
+        return rs
+
+    runs = [] if timed_value else regions(False)
+    truns = regions(True)
+    ctx.service_set_timing(True)
+    if timed_value:
+        runs = truns
     runs.sort(key=lambda r: r[0])
-    svc_el, per_rank, grid_ms, mhz, _ = runs[len(runs) // 2]
+    truns_s = sorted(truns, key=lambda r: r[2])
+    svc_el, per_rank, _, mhz, _ = runs[len(runs) // 2]
+    grid_ms = truns_s[len(truns_s) // 2][2]
     out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
                 "svc_all_ms": [round(r[0] * 1e3, 4) for r in runs],
-                "svc_all_grid_ms": [round(r[2], 4) for r in runs],
-                "svc_all_call_us": [round(r[4], 1) for r in runs]})
+                "svc_all_call_us": [round(r[4], 1) for r in runs],
+                "svc_timed_regions_ms": [round(r[0] * 1e3, 4) for r in truns],
+                "svc_all_grid_ms": [round(r[2], 4) for r in truns],
+                "svc_value_regions": "timed with dispatch events" if timed_value else "no timing events"})
     return out
 
 
@@ -832,11 +852,12 @@ def run_hf(args, W):
     elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
     bytes_per_batch = BYTES_PER_PACKET * n
     if headline == "service":
-        achieved = bytes_per_batch * args.steps / (max(m["grid_ms"], 1e-9) * 1e-3) / 1e9   # 0: HFV_SVC_NOEV
+        achieved = bytes_per_batch * args.steps / (m["grid_ms"] * 1e-3) / 1e9
         kern = {"kernel": "k_verify_service", "grid_ms": round(m["grid_ms"], 4), "batches_per_grid": args.steps,
                 "kernel_ms_per_batch": round(m["grid_ms"] / args.steps, 5),
                 "algorithmic_bytes_per_batch": int(bytes_per_batch),
-                "timing": "dispatch start/stop events of the service grid (hipExtLaunchKernel) over all K batches"}
+                "timing": "dispatch start/stop events of the service grid (hipExtLaunchKernel) over all K batches, "
+                          "in timed regions identical to the value's but for the events (median grid)"}
         traffic = pmc_traffic(f"svc:{args.keysel}:{n}:rot{args.rotate}")
     else:
         achieved = bytes_per_batch / (m["k_mean"] * 1e-3) / 1e9
@@ -881,6 +902,7 @@ def run_hf(args, W):
             "ms_per_step": round(m["svc_el"] / args.steps * 1e3, 5), "grid_ms": round(m["grid_ms"], 4),
             "shader_mhz": round(m["mhz"], 1) if m["mhz"] else None,
             "timed_regions_ms": m.get("svc_all_ms"), "grids_ms": m.get("svc_all_grid_ms"),
+            "event_timed_regions_ms": m.get("svc_timed_regions_ms"), "value_regions": m.get("svc_value_regions"),
             "service_run_call_us": m.get("svc_all_call_us"),
             "note": f"value = the median of {args.svc_reps} timed regions of K steps each (each a fresh grid)"},
         "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),

@@ -233,6 +233,11 @@ int hfv_service_wait(hfv_ctx *ctx, uint64_t ticket, int timeout_ms);
  * lifetime (dispatch start/stop events).  -ETIMEDOUT if it had exited on its idle timeout. */
 int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms);
 int hfv_service_running(const hfv_ctx *ctx);
+/* Grids started from now on carry the dispatch start/stop events that hfv_service_stop /
+ * hfv_service_run report as the lifetime (1, the default) or not (0: the lifetime reads 0).
+ * The events cost the runtime ~12 us per launch-to-synchronize round trip on MI355X (7.5 us of
+ * host time in the launch call, profiles/r03/launch_cost/), which a short run can leave out. */
+int hfv_service_set_timing(hfv_ctx *ctx, int enable);
 
 /* ---- key-schedule kernels ------------------------------------------------------------
  * AES-128 key expansion + CMAC K1 on the GPU, one key per lane: device raw keys[n] ->

@@ -242,6 +242,8 @@ struct hfv_ctx {
     std::vector<uint64_t> svc_lost;  // tickets of stopped grids that were never verified (bounded)
     uint64_t svc_tag = 0;            // generation of the running grid << 40 (see s_svc_tag)
     bool svc_stop_posted = false;    // the running grid's stop descriptor is already in the ring
+    bool svc_timing = true;          // launch grids with dispatch start/stop events (hfv_service_set_timing)
+    bool svc_timed = false;          // ... the running / last grid was
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
 };
 
@@ -1542,14 +1544,6 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
     return 0;
 }
 
-// Diagnostics: HFV_SVC_NOEV=1 launches the service grid without the dispatch start/stop events
-// (its lifetime then reads 0 ms) -- to measure what the events cost a timed region.
-static bool svc_noev()
-{
-    static const bool v = getenv("HFV_SVC_NOEV") && atoi(getenv("HFV_SVC_NOEV"));
-    return v;
-}
-
 static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
 {
     if (kernel_ms) *kernel_ms = 0.0f;
@@ -1579,7 +1573,7 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     ctx->svc_running = false;
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;
-    if (kernel_ms && !svc_noev()) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
+    if (kernel_ms && ctx->svc_timed) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
     // A grid that left on the stop descriptor verified every batch before it (each block
     // reaches the stop only after its share of all earlier batches).  An idle or watchdog
     // exit is clean unless it left a posted batch unverified (batches may complete out of
@@ -1655,7 +1649,8 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
 
 static int svc_launch(hfv_ctx *ctx, DevState *ds)
 {
-    const bool noev = svc_noev();
+    const bool noev = !ctx->svc_timing;
+    ctx->svc_timed = !noev;
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
                                   ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream,
                                   noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
@@ -1874,6 +1869,13 @@ int hfv_service_stop(hfv_ctx *ctx, float *kernel_ms)
 }
 
 int hfv_service_running(const hfv_ctx *ctx) { return ctx && ctx->svc_running ? 1 : 0; }
+
+int hfv_service_set_timing(hfv_ctx *ctx, int enable)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    ctx->svc_timing = enable != 0;
+    return 0;
+}
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
 // 0 loaded ring slot i's descriptor (i < kSvcRing); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and

@@ -122,6 +122,7 @@ def lib():
         "hfv_memcpy_d2h": (i32, [vp, vp, vp, sz]),
         "hfv_last_error": (ctypes.c_char_p, []),
         "hfv_abi_version": (i32, []),
+        "hfv_service_set_timing": (i32, [vp, i32]),
         "aes_key_expansion": (None, [vp, vp]),
         "aes_cypher": (i32, [vp, vp, vp]),
         "aes_cmac_subkeys": (None, [vp, vp]),
@@ -557,6 +558,10 @@ class Ctx:
         us = lambda t: round((int(t) - r0) / 100.0, 2) if t else None   # noqa: E731
         return {"loop_us": us(r1), "relay_us": [us(clk[SVC_RING + 4 + i]) for i in range(nbatches + 1)],
                 "load_us": [us(clk[i]) for i in range(nbatches + 1)]}
+
+    def service_set_timing(self, enable):
+        """Launch later service grids with (True) or without the dispatch timing events."""
+        _check(lib().hfv_service_set_timing(self._h, 1 if enable else 0))
 
     @property
     def service_running(self):

@@ -7,10 +7,10 @@ OUT=gpurun_out/${1:-r03_overhead}
 mkdir -p $OUT
 ARGS="--steps 20 --warmup 5 --no-extras --no-host-e2e --cpu-budget 0 --loop-n 0 --svc-reps 5"
 for i in 1 2 3; do
-    for v in base noev devkernarg skipargcopy nodirect; do
+    for v in untimed timed; do
         case $v in
-            base) E="" ;;
-            noev) E="HFV_SVC_NOEV=1" ;;
+            untimed) E="HFV_BENCH_TIMED_VALUE=0" ;;
+            timed) E="HFV_BENCH_TIMED_VALUE=1" ;;
             devkernarg) E="HIP_FORCE_DEV_KERNARG=1" ;;
             skipargcopy) E="ROC_SKIP_KERNEL_ARG_COPY=1" ;;
             nodirect) E="AMD_DIRECT_DISPATCH=0" ;;
@@ -22,8 +22,9 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 s = d["service"]
 ov = [round((r - g) * 1e3, 1) for r, g in zip(s["timed_regions_ms"], s["grids_ms"])]
+ovt = [round((r - g) * 1e3, 1) for r, g in zip(s["event_timed_regions_ms"], s["grids_ms"])]
 print(f"{sys.argv[2]:12s} value {d['value']:9.1f} ms/step {d['ms_per_step']*1e3:6.2f}us grid/batch {d['roofline']['kernel_ms_per_batch']*1e3:6.2f}us "
-      f"region-grid us {ov} launch us {s['service_run_call_us']} mhz {s['shader_mhz']}")
+      f"value-region - grid us {ov} event-region - grid us {ovt} launch us {s['service_run_call_us']} mhz {s['shader_mhz']}")
 PY
     done
 done

@@ -1651,9 +1651,17 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
 {
     const bool noev = !ctx->svc_timing;
     ctx->svc_timed = !noev;
+    // batch 0 of this grid, if the caller posted it before the launch (svc_run, submitv): in the
+    // kernel arguments as well, so the blocks need not wait for the relay to fetch it
+    SvcFirst first = {0, 0, 0, 0};
+    if (ctx->svc_next > 1) {
+        const SvcDesc &d = ctx->svc_host->desc[0];
+        first = {d.recs, d.bits, d.n, d.n == kSvcStopN ? 1u : d.stride};
+    }
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
-                                  ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, ctx->svc_stream,
-                                  noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
+                                  ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, first,
+                                  ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1],
+                                  &ctx->svc_grid);
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ctx->svc_running = true;

@@ -170,10 +170,15 @@ int build_ttab_image(uint32_t *img, void *stream);
 // persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
 // block waits for the next descriptor before it exits with status kSvcIdleTimeout
 // returns the grid size in *grid
+// The first batch travels in the kernel arguments too (stride 0: none posted before launch), so
+// every block starts on it without waiting for the relay's PCIe round trips.
+struct SvcFirst {
+    uint64_t recs, bits, n, stride;
+};
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
-                          void *ev_stop, unsigned *grid);
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, void *stream,
+                          void *ev_start, void *ev_stop, unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

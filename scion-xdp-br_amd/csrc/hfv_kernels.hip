@@ -877,6 +877,30 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
     return true;
 }
 
+// Batch 0 from the kernel arguments (SvcFirst): the slot svc_load would fill from the mirror,
+// filled before the prologue barrier by one thread of every block.
+__device__ void svc_load_first(SvcShared *host, const SvcFirst &f)
+{
+    SvcSlot &s = s_svc[0];
+    s.base = 0;
+    s.done = 0;
+    s.recs = f.recs;
+    s.bits = f.bits;
+    s.stride = f.stride;
+    s.stop = f.n == kSvcStopN;
+    if (s.stop) {
+        s.count = 0;
+    } else {
+        const uint64_t ntiles = (f.n + 63) / 64;
+        const uint64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+        s.n = f.n;
+        s.tile0 = t0;
+        s.count = (uint32_t)(t1 - t0);
+        if (s.count == 0) svc_complete(host, 0);
+    }
+    s_svc_loaded = 1;
+}
+
 // The wave has just entered batch b: if batch b + 1 is not loaded yet and nobody is loading,
 // take one look for its descriptor now, so the block's waves find it loaded when they reach
 // the end of batch b instead of waiting a PCIe round trip there.
@@ -978,7 +1002,7 @@ template <int KEYSEL, int TAB>
 __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__restrict__ tab,
                                                          const uint32_t *__restrict__ ttab_img, SvcShared *host,
                                                          SvcDesc *mir, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t idle_ticks, uint64_t tag)
+                                                         uint64_t idle_ticks, uint64_t tag, SvcFirst first)
 {
     const uint32_t lane = threadIdx.x & 63;
     UniformKey ukey(tab);
@@ -987,6 +1011,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         s_svc_loaded = 0;
         s_svc_lock = 0;
         s_svc_tag = tag;
+        if (first.stride) svc_load_first(host, first);   // batch 0 without waiting for the relay
     }
     // Block 0's last wave relays the host's descriptors into device memory for the grid's
     // whole life.  It must not be alive at a barrier the other waves wait at (a wave still
@@ -1168,8 +1193,8 @@ int launch_debug_spin(void *stream, uint32_t us)
 
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, void *stream, void *ev_start,
-                          void *ev_stop, unsigned *grid_out)
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, void *stream,
+                          void *ev_start, void *ev_stop, unsigned *grid_out)
 {
     // Per-interface keys (config 3).  Default: three LDS rows per slot beside all four round
     // tables, rounds 3..10's keys expanded per packet (SchedKey): bank-conflict cycles 1.37 M ->
@@ -1190,7 +1215,7 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     *grid_out = grid;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, host, mir, inf_off, hf_off,
-                          idle_ticks, tag);
+                          idle_ticks, tag, first);
     return (int)hipGetLastError();
 }
 

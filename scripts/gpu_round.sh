@@ -18,7 +18,7 @@ step() {   # step <name> <timeout-s> <cmd...>
 }
 MODE=${1:-all}
 if [[ $MODE == all || $MODE == test ]]; then
-    step pytest_gpu 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+    step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
     rc=$?
     # 1 = some test failed (read the log); anything else non-zero = crash/timeout: stop here
     if [[ $rc -gt 1 ]]; then exit $rc; fi

@@ -1885,6 +1885,22 @@ int hfv_service_set_timing(hfv_ctx *ctx, int enable)
     return 0;
 }
 
+// Diagnostic (not part of include/scion_hfv.h; HFV_SVC_SPAN builds fill it): the last grid's
+// block entry stamps (grid words), table-fill stamps (grid words) and wave exit stamps (grid *
+// 16 words, block * 16 + wave; 0 for a wave that did not run the loop), s_memrealtime (100 MHz).
+int hfv_debug_service_span(hfv_ctx *ctx, uint64_t *out, size_t words)
+{
+    if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
+    const size_t g = ctx->svc_grid;
+    if (words < g * 18) return fail(-EINVAL, "need %zu words", g * 18);
+    for (size_t i = 0; i < g; ++i) {
+        out[i] = __atomic_load_n(&ctx->svc_host->span_entry[i], __ATOMIC_ACQUIRE);
+        out[g + i] = __atomic_load_n(&ctx->svc_host->span_fill[i], __ATOMIC_ACQUIRE);
+    }
+    for (size_t i = 0; i < g * 16; ++i) out[2 * g + i] = __atomic_load_n(&ctx->svc_host->span_exit[i], __ATOMIC_ACQUIRE);
+    return 0;
+}
+
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
 // 0 loaded ring slot i's descriptor (i < kSvcRing); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and
 // s_memrealtime at its start and at its exit (the shader clock over the grid's life);

@@ -120,6 +120,11 @@ struct SvcShared {
     uint64_t run_clock[4];           // diagnostics: block 0 wave 0 s_memtime/s_memrealtime at start, at exit
     uint64_t relay_clock[kSvcRing];  // diagnostics: s_memrealtime when the relay published the slot
     uint64_t prof[8];                // diagnostics (HFV_SVC_PROF builds): shader cycles per loop phase, summed over waves
+    // diagnostics (HFV_SVC_SPAN builds): s_memrealtime at each block's entry and after its table
+    // fill, and at each wave's exit (block * 16 + wave)
+    uint64_t span_entry[kSvcMaxBlocks];
+    uint64_t span_fill[kSvcMaxBlocks];
+    uint64_t span_exit[kSvcMaxBlocks * 16];
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;

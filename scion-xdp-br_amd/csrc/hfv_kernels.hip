@@ -720,6 +720,11 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 #ifndef HFV_SVC_PROF
 #define HFV_SVC_PROF 0
 #endif
+// HFV_SVC_SPAN = 1: diagnostic build; block entry, table-fill and wave exit stamps
+// (s_memrealtime, 100 MHz) into host->span_* (hfv_debug_service_span)
+#ifndef HFV_SVC_SPAN
+#define HFV_SVC_SPAN 0
+#endif
 // Only wave 1 of every block samples (s_memtime from every wave of a CU slowed the loop
 // many times over); the other waves run the plain loop beside it.
 struct SvcProf {
@@ -1005,6 +1010,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
                                                          uint64_t idle_ticks, uint64_t tag, SvcFirst first)
 {
     const uint32_t lane = threadIdx.x & 63;
+    if (HFV_SVC_SPAN && threadIdx.x == 0)
+        __hip_atomic_store(&host->span_entry[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     UniformKey ukey(tab);
     if (threadIdx.x == 0) {
         s_svc_next = 0;
@@ -1029,6 +1037,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if (!relay) fill_keys3(tab, nthr);
     }
     __syncthreads();
+    if (HFV_SVC_SPAN && threadIdx.x == 0)
+        __hip_atomic_store(&host->span_fill[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     if (relay) {   // no barrier follows: the block's other waves go on without it
         if (lane == 0) svc_relay(host, mir, idle_ticks, tag);
         return;
@@ -1169,6 +1180,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         rc = rn;
     }
     prof.flush(host, lane, prof_t0);
+    if (HFV_SVC_SPAN && lane == 0)
+        __hip_atomic_store(&host->span_exit[blockIdx.x * 16 + (threadIdx.x >> 6)], __builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         __hip_atomic_store(&host->run_clock[2], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&host->run_clock[3], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,

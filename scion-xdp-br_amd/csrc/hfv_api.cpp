@@ -245,6 +245,13 @@ struct hfv_ctx {
     bool svc_timing = true;          // launch grids with dispatch start/stop events (hfv_service_set_timing)
     bool svc_timed = false;          // ... the running / last grid was
     hipEvent_t svc_ev[2] = {nullptr, nullptr};
+    // work balance across the grid's blocks (SvcWeights, svc_balance)
+    SvcWeights svc_w = {{kSvcWeightUnit, kSvcWeightUnit, kSvcWeightUnit, kSvcWeightUnit, kSvcWeightUnit,
+                         kSvcWeightUnit, kSvcWeightUnit, kSvcWeightUnit},
+                        kSvcWeightUnit, {0, 0, 0}};
+    SvcWeights svc_w_used = svc_w;   // the running / last grid's
+    bool svc_adapt = false;          // the running grid got all its batches up front (svc_run): measure it
+    std::vector<uint64_t> svc_run_ns;   // ... their record counts
 };
 
 static int device_numa(int device, cpu_set_t *cpus);
@@ -1544,6 +1551,59 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
     return 0;
 }
 
+// Re-derive the block weights from the grid that just stopped (svc_run grids only: every batch
+// was posted before the launch, so no block waited for the host and a block's tiles over its
+// time from table fill to its last completed share is its verify rate).  Weights follow the
+// XCDs' mean rates (block j on XCD j % 8) and block 0's own, averaged with the previous weights
+// (halves run-to-run noise), clamped to [1/2, 2] of nominal.  Grids shorter than 50 us carry
+// too little signal and leave them alone.  HFV_SVC_BALANCE=0 keeps equal shares.
+static void svc_balance(hfv_ctx *ctx)
+{
+    static const bool off = getenv("HFV_SVC_BALANCE") && !strcmp(getenv("HFV_SVC_BALANCE"), "0");
+    const uint64_t G = ctx->svc_grid;
+    if (off || G < 16 || ctx->svc_run_ns.empty()) return;
+    const SvcWeights &wu = ctx->svc_w_used;
+    std::vector<uint64_t> cum(G + 1, 0);
+    for (uint64_t k = 0; k < G; ++k) cum[k + 1] = cum[k] + (k ? wu.w[k % 8] : wu.w0);
+    const uint64_t W = cum[G];
+    std::vector<double> tiles(G, 0.0);
+    for (size_t i = 0; i < ctx->svc_run_ns.size();) {   // runs of equal batch sizes at once
+        size_t j = i;
+        while (j < ctx->svc_run_ns.size() && ctx->svc_run_ns[j] == ctx->svc_run_ns[i]) ++j;
+        const uint64_t T = (ctx->svc_run_ns[i] + 63) / 64;
+        for (uint64_t k = 0; k < G; ++k)
+            tiles[k] += (double)(j - i) * (double)(T * cum[k + 1] / W - T * cum[k] / W);
+        i = j;
+    }
+    double rx[8] = {0}, r0 = 0, rsum = 0;
+    int cx[8] = {0};
+    uint64_t span = 0;
+    for (uint64_t k = 0; k < G; ++k) {
+        const uint64_t a = __atomic_load_n(&ctx->svc_host->blk_start[k], __ATOMIC_ACQUIRE);
+        const uint64_t b = __atomic_load_n(&ctx->svc_host->blk_fin[k], __ATOMIC_ACQUIRE);
+        if (b <= a || tiles[k] <= 0) return;   // a block without a measurement: keep the weights
+        if (b - a > span) span = b - a;
+        const double r = tiles[k] / (double)(b - a);
+        rsum += r;
+        if (k == 0) r0 = r;
+        else {
+            rx[k % 8] += r;
+            cx[k % 8] += 1;
+        }
+    }
+    if (span < 5000) return;   // 100 MHz ticks: 50 us
+    const double mean = rsum / (double)G;
+    auto blend = [&](uint32_t old, double rate) {
+        double w = 0.5 * old + 0.5 * kSvcWeightUnit * rate / mean;
+        if (w < kSvcWeightUnit / 2) w = kSvcWeightUnit / 2;
+        if (w > kSvcWeightUnit * 2) w = kSvcWeightUnit * 2;
+        return (uint32_t)(w + 0.5);
+    };
+    for (int x = 0; x < 8; ++x)
+        if (cx[x]) ctx->svc_w.w[x] = blend(ctx->svc_w.w[x], rx[x] / cx[x]);
+    ctx->svc_w.w0 = blend(ctx->svc_w.w0, r0);
+}
+
 static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
 {
     if (kernel_ms) *kernel_ms = 0.0f;
@@ -1574,6 +1634,8 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;
     if (kernel_ms && ctx->svc_timed) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
+    if (ctx->svc_adapt && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) svc_balance(ctx);
+    ctx->svc_adapt = false;
     // A grid that left on the stop descriptor verified every batch before it (each block
     // reaches the stop only after its share of all earlier batches).  An idle or watchdog
     // exit is clean unless it left a posted batch unverified (batches may complete out of
@@ -1644,6 +1706,7 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
     ctx->svc_next = 1;
     ctx->svc_base = ctx->svc_ticket;
     ctx->svc_stop_posted = false;
+    ctx->svc_adapt = false;
     return 0;
 }
 
@@ -1658,9 +1721,10 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
         const SvcDesc &d = ctx->svc_host->desc[0];
         first = {d.recs, d.bits, d.n, d.n == kSvcStopN ? 1u : d.stride};
     }
+    ctx->svc_w_used = ctx->svc_w;
     int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
                                   ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, first,
-                                  ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1],
+                                  ctx->svc_w_used, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1],
                                   &ctx->svc_grid);
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
@@ -1804,6 +1868,9 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
     DevState *ds;
     rc = svc_begin(ctx, ctx->svc_idle_ms, &ds);
     if (rc) return rc;
+    ctx->svc_adapt = true;   // every batch is in the ring before the grid starts: measure its balance
+    ctx->svc_run_ns.resize(count);
+    for (size_t i = 0; i < count; ++i) ctx->svc_run_ns[i] = batches[i].n;
     clock_gettime(CLOCK_MONOTONIC, &t_beg);
     // the batches, then the stop right behind them, are in the ring before the grid starts (a
     // longer run launches once the ring is full): the grid exits as soon as its blocks finish
@@ -1882,6 +1949,16 @@ int hfv_service_set_timing(hfv_ctx *ctx, int enable)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     ctx->svc_timing = enable != 0;
+    return 0;
+}
+
+// Diagnostic (not part of include/scion_hfv.h): the block weights the next service grid will
+// use (w[0..7] per XCD, then block 0's), in units of 1/1024 of an equal share.
+int hfv_debug_service_weights(hfv_ctx *ctx, uint32_t out[9])
+{
+    if (!ctx || !out) return fail(-EINVAL, "bad argument");
+    for (int x = 0; x < 8; ++x) out[x] = ctx->svc_w.w[x];
+    out[8] = ctx->svc_w.w0;
     return 0;
 }
 

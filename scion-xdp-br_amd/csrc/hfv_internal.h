@@ -125,6 +125,10 @@ struct SvcShared {
     uint64_t span_entry[kSvcMaxBlocks];
     uint64_t span_fill[kSvcMaxBlocks];
     uint64_t span_exit[kSvcMaxBlocks * 16];
+    // work balance (SvcWeights): s_memrealtime when block k finished its table fill, and when it
+    // last completed its share of a batch
+    uint64_t blk_start[kSvcMaxBlocks];
+    uint64_t blk_fin[kSvcMaxBlocks];
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
@@ -180,10 +184,33 @@ int build_ttab_image(uint32_t *img, void *stream);
 struct SvcFirst {
     uint64_t recs, bits, n, stride;
 };
+// Work balance of the resident grid.  The XCDs of one MI355X do not verify at the same rate
+// (per-XCD means of the blocks' finish times differ by up to ~12 us over a 0.24 ms grid,
+// profiles/r03/svc_span_*.log), and the grid ends with its slowest block.  Block k's share of a
+// batch of T tiles is [T*cum(k)/W, T*cum(k+1)/W), W = cum(G), where cum(k) sums the weights of
+// blocks 0..k-1: block j weighs w[j % 8] (workgroups go round the 8 XCDs in order), block 0
+// (which also runs the relay wave) w0.  Equal weights give the plain T*k/G split.  The host
+// re-derives the weights from each block's measured rate after every hfv_service_run grid.
+struct SvcWeights {
+    uint32_t w[8];
+    uint32_t w0;
+    uint32_t pad[3];
+};
+constexpr uint32_t kSvcWeightUnit = 1024;
+constexpr uint64_t svc_cum(const SvcWeights &sw, uint64_t k)
+{
+    if (k == 0) return 0;
+    uint64_t all = 0, part = 0;
+    for (uint64_t x = 0; x < 8; ++x) {
+        all += sw.w[x];
+        if (x < k % 8) part += sw.w[x];
+    }
+    return (k / 8) * all + part - sw.w[0] + sw.w0;
+}
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, void *stream,
-                          void *ev_start, void *ev_stop, unsigned *grid);
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, SvcWeights weights,
+                          void *stream, void *ev_start, void *ev_stop, unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

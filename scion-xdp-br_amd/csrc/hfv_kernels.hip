@@ -676,6 +676,13 @@ static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
 // mirror and the completion words carry tag | ticket, so words a previous grid left behind
 // never match and nothing has to be cleared between grids.
 static __shared__ uint64_t s_svc_tag;
+// This block's share bounds (SvcWeights): tiles [T * s_svc_c0 / s_svc_w, T * s_svc_c1 / s_svc_w).
+static __shared__ uint64_t s_svc_c0, s_svc_c1, s_svc_w;
+__device__ __forceinline__ void svc_share(uint64_t ntiles, uint64_t &t0, uint32_t &count)
+{
+    t0 = ntiles * s_svc_c0 / s_svc_w;
+    count = (uint32_t)(ntiles * s_svc_c1 / s_svc_w - t0);
+}
 
 struct SvcTile {   // one claimed tile, wave-uniform
     uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + (g - base)
@@ -767,6 +774,8 @@ struct SvcProf {
 // at the memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/).
 __device__ void svc_complete(SvcShared *host, uint32_t b)
 {
+    __hip_atomic_store(&host->blk_fin[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&host->done[b % kSvcRing][blockIdx.x], s_svc_tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -871,11 +880,12 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
     if (stop) {
         s.count = 0;
     } else {
-        const uint64_t ntiles = (n + 63) / 64;
-        const uint64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+        uint64_t t0;
+        uint32_t cnt;
+        svc_share((n + 63) / 64, t0, cnt);
         s.n = n;
         s.tile0 = t0;
-        s.count = (uint32_t)(t1 - t0);
+        s.count = cnt;
         if (s.count == 0) svc_complete(host, b);
     }
     __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -896,11 +906,12 @@ __device__ void svc_load_first(SvcShared *host, const SvcFirst &f)
     if (s.stop) {
         s.count = 0;
     } else {
-        const uint64_t ntiles = (f.n + 63) / 64;
-        const uint64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+        uint64_t t0;
+        uint32_t cnt;
+        svc_share((f.n + 63) / 64, t0, cnt);
         s.n = f.n;
         s.tile0 = t0;
-        s.count = (uint32_t)(t1 - t0);
+        s.count = cnt;
         if (s.count == 0) svc_complete(host, 0);
     }
     s_svc_loaded = 1;
@@ -1007,7 +1018,8 @@ template <int KEYSEL, int TAB>
 __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__restrict__ tab,
                                                          const uint32_t *__restrict__ ttab_img, SvcShared *host,
                                                          SvcDesc *mir, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t idle_ticks, uint64_t tag, SvcFirst first)
+                                                         uint64_t idle_ticks, uint64_t tag, SvcFirst first,
+                                                         SvcWeights weights)
 {
     const uint32_t lane = threadIdx.x & 63;
     if (HFV_SVC_SPAN && threadIdx.x == 0)
@@ -1019,6 +1031,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         s_svc_loaded = 0;
         s_svc_lock = 0;
         s_svc_tag = tag;
+        s_svc_c0 = svc_cum(weights, blockIdx.x);
+        s_svc_c1 = svc_cum(weights, blockIdx.x + 1);
+        s_svc_w = svc_cum(weights, gridDim.x);
         if (first.stride) svc_load_first(host, first);   // batch 0 without waiting for the relay
     }
     // Block 0's last wave relays the host's descriptors into device memory for the grid's
@@ -1037,6 +1052,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if (!relay) fill_keys3(tab, nthr);
     }
     __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&host->blk_start[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     if (HFV_SVC_SPAN && threadIdx.x == 0)
         __hip_atomic_store(&host->span_fill[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1207,8 +1225,8 @@ int launch_debug_spin(void *stream, uint32_t us)
 
 int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
                           uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, void *stream,
-                          void *ev_start, void *ev_stop, unsigned *grid_out)
+                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, SvcWeights weights,
+                          void *stream, void *ev_start, void *ev_stop, unsigned *grid_out)
 {
     // Per-interface keys (config 3).  Default: three LDS rows per slot beside all four round
     // tables, rounds 3..10's keys expanded per packet (SchedKey): bank-conflict cycles 1.37 M ->
@@ -1229,7 +1247,7 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     *grid_out = grid;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, host, mir, inf_off, hf_off,
-                          idle_ticks, tag, first);
+                          idle_ticks, tag, first, weights);
     return (int)hipGetLastError();
 }
 

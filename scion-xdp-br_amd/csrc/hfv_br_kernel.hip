@@ -60,6 +60,17 @@ static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 #ifndef HFV_BR_PROF
 #define HFV_BR_PROF 0
 #endif
+// HFV_BR_WB: order of a tile's write-back against the next tile's header loads.
+//   0: stores, then the next tile's loads at the top of the loop (vmcnt retires in order, so
+//      the wait for the loads also waits for the stores' acknowledgement);
+//   1: the changed chunks are read from LDS into registers, the next tile's loads are issued,
+//      then the chunks go out as buffer stores whose lanes without a change address past the
+//      tile's buffer range (dropped by the bounds check: no branch, a fixed count of stores), and
+//      the loop waits for the loads only (vmcnt = that count);
+//   9: diagnostic, no write-back at all (wrong output: measures what the stores cost).
+#ifndef HFV_BR_WB
+#define HFV_BR_WB 1
+#endif
 #if HFV_BR_PROF
 __device__ unsigned long long g_br_prof[8];
 #endif
@@ -146,12 +157,19 @@ __device__ __forceinline__ uint32_t lds_u32_at(const BrFrame &k, int off)
     int a = off >> 2;
     return __builtin_amdgcn_alignbyte(row[a + 1], row[a], (uint32_t)(off & 3));
 }
+// The wait for a read past the window sits inside its branch: placed after the merge by the
+// waitcnt pass, a vmcnt(0) would run on every path and wait for the previous tile's write-back
+// stores, which vmcnt retires in order before this read (HFV_BR_WB == 1 leaves them in flight).
+__device__ __forceinline__ void wait_past_window() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
 __device__ __forceinline__ uint32_t rd8(const BrFrame &k, int off)
 {
     if (k.win == 0) return g8(k.p + off);
     const bool in = (uint32_t)off < (uint32_t)k.win;
     uint32_t v = reinterpret_cast<const uint8_t *>(s_hdr + k.row)[in ? off : 0];
-    if (!in) v = g8(k.p + off);
+    if (!in) {
+        v = g8(k.p + off);
+        wait_past_window();
+    }
     return v;
 }
 __device__ __forceinline__ uint32_t rd16(const BrFrame &k, int off)
@@ -159,7 +177,10 @@ __device__ __forceinline__ uint32_t rd16(const BrFrame &k, int off)
     if (k.win == 0) return g16(k.p + off);
     const bool in = (uint32_t)off + 2 <= (uint32_t)k.win;
     uint32_t v = lds_u32_at(k, in ? off : 0) & 0xffffu;
-    if (!in) v = g16(k.p + off);
+    if (!in) {
+        v = g16(k.p + off);
+        wait_past_window();
+    }
     return v;
 }
 __device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
@@ -167,7 +188,10 @@ __device__ __forceinline__ uint32_t rd32(const BrFrame &k, int off)
     if (k.win == 0) return g32(k.p + off);
     const bool in = (uint32_t)off + 4 <= (uint32_t)k.win;
     uint32_t v = lds_u32_at(k, in ? off : 0);
-    if (!in) v = g32(k.p + off);
+    if (!in) {
+        v = g32(k.p + off);
+        wait_past_window();
+    }
     return v;
 }
 
@@ -763,7 +787,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     // Tiles go round the blocks first (wave w of block b starts at tile w * grid + b), so a
     // launch of fewer tiles than waves (the config-5 loop's 64 Ki-frame chunks: 1024 tiles)
     // still spreads over every CU instead of filling a quarter of them with 16 waves each.
-    uint64_t t = (uint64_t)wib * gridDim.x + blockIdx.x;
+    // (wave-uniform as far as the compiler knows: the buffer resources built from it stay in SGPRs)
+    uint64_t t = (uint64_t)__builtin_amdgcn_readfirstlane(wib) * gridDim.x + blockIdx.x;
     if (s_br.detached) {   // `hfv-loader detach`: no router on the interface, every frame goes up the stack
         for (; t < ntiles; t += nwaves) {
             const uint64_t i = t * 64 + lane;
@@ -798,10 +823,43 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
         pre_len = lens[fi];
         pre_ifx = ifidx[fi];
     };
+    // HFV_BR_WB == 1: the same loads as buffer loads from a wave-uniform tile base (one lane
+    // offset for all C chunks; lanes past the batch read zeros instead of a clamped frame)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t voff = fr_of * (uint32_t)slot + 16u * ch;
+    auto fetch_buf = [&](uint64_t tt) {
+        // past the last tile: a zero-sized range (every load returns zeros, no memory access), so
+        // the loop can issue the next tile's loads unconditionally
+        const uint64_t left = tt * 64 < n ? n - tt * 64 : 0;
+        const uint32_t nf = left < 64 ? (uint32_t)left : 64u;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(pkts) + tt * 64 * slot, 0, (int)(nf * (uint32_t)slot), 0x00020000);
+#pragma unroll
+        for (int r = 0; r < C; ++r) {
+            // the whole offset in the VGPR: the bounds check does not cover soffset
+            const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + r * (64 / C) * (uint32_t)slot), 0, 0);
+            pre[r] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        uint64_t fi = tt * 64 + lane;
+        if (fi >= n) fi = n - 1;
+        pre_len = lens[fi];
+        pre_ifx = ifidx[fi];
+    };
     BrProf prof;
+    constexpr bool kEarly = WIN > 0 && HFV_BR_WB == 1;
+    if constexpr (kEarly) {
+        if (t < ntiles) fetch_buf(t);
+        // (a builtin, so the waitcnt pass knows: the loop's vmcnt(C) assumes C younger stores)
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+    }
     for (; t < ntiles; t += nwaves) {
         prof.start();
-        fetch(t);
+        if constexpr (!kEarly) fetch(t);
+        if constexpr (kEarly) {
+            // the loads of this tile were issued at the end of the previous one, before its C
+            // write-back stores: wait for everything but those stores
+            __builtin_amdgcn_s_waitcnt(0x0F70 | C);   // vmcnt(C) expcnt(7) lgkmcnt(15)
+        }
         if constexpr (WIN > 0) {
             uint32_t *rows = s_hdr + wib * 64 * kBrRow;
 #pragma unroll
@@ -842,12 +900,28 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t *rows = s_hdr + wib * 64 * kBrRow;
+            if constexpr (HFV_BR_WB == 1) {
+                // the next tile's loads go to registers (the rows are read below, then restaged at
+                // the top of the next iteration), ahead of this tile's stores
+                fetch_buf(t + nwaves);
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(out + t * 64 * slot, 0, (int)(64u * (uint32_t)slot), 0x00020000);
 #pragma unroll
-            for (int r = 0; r < C; ++r) {
-                uint32_t fr = r * (64 / C) + fr_of;
-                if ((cmask[r] >> ch) & 1u) {
+                for (int r = 0; r < C; ++r) {
+                    const uint32_t fr = r * (64 / C) + fr_of;
                     const uint32_t *q = rows + fr * kBrRow + 4 * ch;
-                    *reinterpret_cast<uint4 *>(out + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
+                    const v4u q4 = v4u{q[0], q[1], q[2], q[3]};
+                    const uint32_t off = ((cmask[r] >> ch) & 1u) ? voff + r * (64 / C) * (uint32_t)slot : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(q4, rs, (int)off, 0, 0);
+                }
+            } else if constexpr (HFV_BR_WB == 0) {
+#pragma unroll
+                for (int r = 0; r < C; ++r) {
+                    uint32_t fr = r * (64 / C) + fr_of;
+                    if ((cmask[r] >> ch) & 1u) {
+                        const uint32_t *q = rows + fr * kBrRow + 4 * ch;
+                        *reinterpret_cast<uint4 *>(out + (t * 64 + fr) * slot + 16 * ch) = make_uint4(q[0], q[1], q[2], q[3]);
+                    }
                 }
             }
         }

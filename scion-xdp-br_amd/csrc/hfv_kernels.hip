@@ -732,6 +732,14 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 #ifndef HFV_SVC_SPAN
 #define HFV_SVC_SPAN 0
 #endif
+// HFV_SVC_AHEAD = 1: the next tile's number is claimed one iteration early (a wave then holds
+// three tiles: the one it computes, the one whose records are loading, the claimed one); 0 (the
+// default): it is claimed at the top of the iteration that loads its records, so a wave holds
+// two and the block's last tiles go to whichever waves are free one tile-time later: K = 20
+// grids 2.1-2.4 % shorter (profiles/r03/ahead_ab/), the claim's LDS latency is not missed.
+#ifndef HFV_SVC_AHEAD
+#define HFV_SVC_AHEAD 0
+#endif
 // Only wave 1 of every block samples (s_memtime from every wave of a CU slowed the loop
 // many times over); the other waves run the plain loop beside it.
 struct SvcProf {
@@ -1076,9 +1084,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     SvcTile none;
     none.base = 0;
     none.count = 0;
-    // The loop, per tile: wait for the tile's records (loaded one iteration ahead), take the
-    // tile number claimed one iteration ago and claim the next (LDS atomic; its latency hides
-    // behind the rounds), store the verdict words of a batch the wave left in the previous
+    // The loop, per tile: wait for the tile's records (loaded one iteration ahead), claim the
+    // next tile (LDS atomic; HFV_SVC_AHEAD = 1 claimed it one iteration earlier still), store the
+    // verdict words of a batch the wave left in the previous
     // iteration (so their write acknowledgement arrives while this tile computes and is
     // covered by the next iteration's wait), map the next tile and issue its loads, compute.
     // Measured with the HFV_SVC_PROF build on the loop this replaces (claim at the top, store
@@ -1091,7 +1099,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     };
     SvcTile cur;
     if (svc_map(host, mir, idle_ticks, lane, wave_uniform(claim()), true, mb, none, cur) != kSvcFound) return;
-    uint32_t gq = claim();   // the next tile's number (lane 0), read one iteration later
+    uint32_t gq = HFV_SVC_AHEAD ? claim() : 0u;   // the next tile's number (lane 0), read one iteration later
     // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
     // out as ONE scattered write-through store, issued at the top of the iteration after the
     // wave left the batch (or filled the stash).  A store per tile would sit in the wave's
@@ -1140,8 +1148,13 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         // (vmcnt retires in order: a row wait must not also wait for those HBM loads)
         GatherKey gk;
         if constexpr (KEYSEL == kKeyselGather) gk.issue(tab, rec_key_slot(rc));
-        const uint32_t g = wave_uniform(gq);
-        gq = claim();
+        uint32_t g;
+        if constexpr (HFV_SVC_AHEAD) {
+            g = wave_uniform(gq);
+            gq = claim();
+        } else {
+            g = wave_uniform(claim());
+        }
         SvcTile nx;
         SvcClaim c = svc_map(host, mir, idle_ticks, lane, g, false, mb, cur, nx);
         if (c != kSvcFound) nx = cur;

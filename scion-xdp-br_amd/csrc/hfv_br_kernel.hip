@@ -71,6 +71,13 @@ static __shared__ uint32_t s_hdr[kBrStageWaves * 64 * kBrRow];
 #ifndef HFV_BR_WB
 #define HFV_BR_WB 1
 #endif
+// HFV_BR_DYN (with HFV_BR_WB == 1): 1 = each block owns a contiguous tile range and its waves
+// claim the next tile from a block-local LDS counter at the end of the current one, so a wave
+// that ran fast takes more; 0 = tile t goes to wave (t mod waves) statically.
+#ifndef HFV_BR_DYN
+#define HFV_BR_DYN 1
+#endif
+static __shared__ uint32_t s_br_next;
 #if HFV_BR_PROF
 __device__ unsigned long long g_br_prof[8];
 #endif
@@ -780,6 +787,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     }
     if constexpr (STATS)
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) s_stats[e] = 0;
+    if (threadIdx.x == 0) s_br_next = 0;
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
@@ -847,12 +855,23 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     };
     BrProf prof;
     constexpr bool kEarly = WIN > 0 && HFV_BR_WB == 1;
+    constexpr bool kDyn = kEarly && HFV_BR_DYN;
+    // kDyn: this block's tiles [tb0, tb1), handed out by s_br_next (ntiles: nothing left)
+    const uint64_t tb0 = ntiles * blockIdx.x / gridDim.x, tb1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    auto claim = [&]() -> uint64_t {
+        uint32_t g = 0;
+        if (lane == 0) g = __hip_atomic_fetch_add(&s_br_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t tt = tb0 + __builtin_amdgcn_readfirstlane(g);
+        return tt < tb1 ? tt : ntiles;
+    };
+    if constexpr (kDyn) t = claim();
+    uint64_t tnext = t + nwaves;
     if constexpr (kEarly) {
         if (t < ntiles) fetch_buf(t);
         // (a builtin, so the waitcnt pass knows: the loop's vmcnt(C) assumes C younger stores)
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
     }
-    for (; t < ntiles; t += nwaves) {
+    for (; t < ntiles; t = kDyn ? tnext : t + nwaves) {
         prof.start();
         if constexpr (!kEarly) fetch(t);
         if constexpr (kEarly) {
@@ -903,7 +922,8 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
             if constexpr (HFV_BR_WB == 1) {
                 // the next tile's loads go to registers (the rows are read below, then restaged at
                 // the top of the next iteration), ahead of this tile's stores
-                fetch_buf(t + nwaves);
+                tnext = kDyn ? claim() : t + nwaves;
+                fetch_buf(tnext);
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(out + t * 64 * slot, 0, (int)(64u * (uint32_t)slot), 0x00020000);
 #pragma unroll

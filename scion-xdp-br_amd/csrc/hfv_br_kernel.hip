@@ -31,8 +31,17 @@
 #ifndef HFV_BR_WAVES
 #define HFV_BR_WAVES 16
 #endif
+// HFV_BR_STATS32 = 1: the block's verdict counters in 32-bit LDS words (5.5 KiB instead of 11),
+// added into the caller's 64-bit counters at the end of the launch; launch_br_process splits a
+// launch so that no block can count 2^32 bytes.  The LDS this frees holds 8 lane copies of the
+// AES tables instead of 4.
+#ifndef HFV_BR_STATS32
+#define HFV_BR_STATS32 1
+#endif
 #ifndef HFV_TAB3_COPIES
-#if HFV_BR_WAVES == 16
+#if HFV_BR_WAVES == 16 && HFV_BR_STATS32
+#define HFV_TAB3_COPIES 8
+#elif HFV_BR_WAVES == 16
 #define HFV_TAB3_COPIES 4
 #else
 #define HFV_TAB3_COPIES 16
@@ -44,7 +53,12 @@
 namespace hfv {
 
 static __shared__ DevBrConfig s_br;
-static __shared__ unsigned long long s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
+#if HFV_BR_STATS32
+typedef uint32_t BrCount;
+#else
+typedef unsigned long long BrCount;
+#endif
+static __shared__ BrCount s_stats[HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS];
 
 // Header staging (WIN > 0 kernels): the first kBrWin bytes of each frame of a wave's 64-frame
 // tile, one row of kBrWin / 4 + 1 dwords per frame (the odd row pitch keeps both the staging
@@ -272,9 +286,9 @@ __device__ __forceinline__ uint32_t record(BrFrame &k, uint32_t verdict)   // re
     if constexpr (STATS) {
         if (k.cut) return verdict & 7u;
         if (k.ifindex < HFV_BR_STATS_IFINDEX && idx < HFV_BR_COUNTERS) {
-            unsigned long long *row = s_stats + k.ifindex * 2 * HFV_BR_COUNTERS;
-            atomicAdd(row + idx, (unsigned long long)k.len);
-            atomicAdd(row + HFV_BR_COUNTERS + idx, 1ull);
+            BrCount *row = s_stats + k.ifindex * 2 * HFV_BR_COUNTERS;
+            atomicAdd(row + idx, (BrCount)k.len);
+            atomicAdd(row + HFV_BR_COUNTERS + idx, (BrCount)1);
         }
     }
     return verdict & 7u;
@@ -961,7 +975,7 @@ __global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict
     if constexpr (STATS) {
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS; e += BLOCK) {
-            unsigned long long v = s_stats[e];
+            unsigned long long v = (unsigned long long)s_stats[e];
             if (v) atomicAdd(stats + e, v);
         }
     }
@@ -984,6 +998,15 @@ static unsigned g_br_grid_override = 0;
 extern "C" int hfv_debug_br_grid(unsigned blocks)
 {
     g_br_grid_override = blocks;
+    return 0;
+}
+// Test-only (hfv_debug_br_split): split launches that count verdicts into pieces of at most
+// `frames` frames (0 = only where 32-bit block counters could overflow), so a test can check
+// that split launches add up to the same counters and outputs.
+static size_t g_br_split_override = 0;
+extern "C" int hfv_debug_br_split(size_t frames)
+{
+    g_br_split_override = frames;
     return 0;
 }
 
@@ -1015,6 +1038,26 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
         block = 1024;
         k = stats ? k_br_process<1024, true, 0> : k_br_process<1024, false, 0>;
     }
+#if HFV_BR_STATS32
+    // 32-bit block counters: split a launch whose blocks could count 2^32 bytes of one kind
+    // (a block's frames x the largest length); every launch adds into the same counters
+    if (stats) {
+        const uint64_t per_block = (uint64_t)(UINT32_MAX / (maxlen ? maxlen : 1));   // frames
+        uint64_t cap_n = (per_block > 64 ? per_block - 64 : 1) * (uint64_t)g.num_cus;   // + a tile of rounding
+        if (g_br_split_override && g_br_split_override < cap_n) cap_n = g_br_split_override;
+        if ((uint64_t)n > cap_n) {
+            for (size_t off = 0; off < n; off += cap_n) {
+                const size_t m = n - off < cap_n ? n - off : (size_t)cap_n;
+                int e = launch_br_process(g, st, pkts + off * slot, slot, maxlen, window, len + off, ingress_ifindex + off, m,
+                                          action + off, verdict + off, egress_ifindex + off, stats, stream,
+                                          off == 0 ? ev_start : nullptr, off + m >= n ? ev_stop : nullptr,
+                                          out + off * slot);
+                if (e) return e;
+            }
+            return 0;
+        }
+    }
+#endif
     const uint64_t tiles = (n + 63) / 64, cap = (uint64_t)g.num_cus;   // one block per CU at most
     unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
     if (g_br_grid_override && g_br_grid_override < grid) grid = g_br_grid_override;

@@ -445,6 +445,12 @@ class Ctx:
         """Test-only: cap k_br_process launches at `blocks` blocks (0 = default geometry)."""
         _check(lib().hfv_debug_br_grid(ctypes.c_uint(blocks)))
 
+    @staticmethod
+    def debug_br_split(frames):
+        """Test-only: split counting k_br_process launches into pieces of at most `frames`
+        frames (0 = only where the 32-bit block counters could overflow)."""
+        _check(lib().hfv_debug_br_split(ctypes.c_size_t(frames)))
+
     def host_register(self, buf):
         _check(lib().hfv_host_register(self._h, _ptr(buf), buf.nbytes))
 

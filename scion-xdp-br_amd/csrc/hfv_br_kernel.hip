@@ -1024,8 +1024,9 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     // forces the direct one).  Persistent grid: one block per CU (LDS: tables + counters
     // [+ header rows]).
     static const int stage_env = getenv("HFV_BR_STAGE") ? atoi(getenv("HFV_BR_STAGE")) : 1;
+    // (the staged loop addresses a tile of 64 slots through 32-bit buffer offsets: 64 * slot < 2^31)
     bool staged = stage_env && slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0 &&
-                  ((uintptr_t)out & 15) == 0;
+                  ((uintptr_t)out & 15) == 0 && slot < ((size_t)1 << 25);
     using K = void (*)(const DevState *, const uint32_t *, const uint8_t *, uint8_t *, uint64_t, uint32_t, uint32_t,
                        const uint16_t *,
                        const uint32_t *, uint64_t, uint8_t *, uint8_t *, int32_t *, unsigned long long *);

@@ -197,15 +197,18 @@ class World:
 
     def timed(self, steps, fn):
         """fn() `steps` times between barrier + device sync on both sides; (max over ranks,
-        per-rank list)."""
+        per-rank list).  Each rank's clock runs from the release of the opening barrier to the
+        end of its closing device synchronize; the closing barrier comes after the clock stops
+        (with RCCL it is itself a collective launch and synchronize, tens of microseconds that are
+        no part of any rank's K steps), and the max over ranks is the job's time."""
         self.barrier()
         self.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             fn()
         self.sync()
-        self.barrier()
         el = time.perf_counter() - t0
+        self.barrier()
         all_el = self.gather(el)
         return max(all_el), all_el
 

@@ -1054,7 +1054,7 @@ def main():
     ap.add_argument("--mode", choices=["service", "launch"], default="service",
                     help="hf headline: resident service grid (default) or one launch per batch")
     ap.add_argument("--settle-s", type=float, default=0.5, help="idle seconds before each extra leg (untimed)")
-    ap.add_argument("--svc-reps", type=int, default=3, help="timed service regions of K steps (median reported)")
+    ap.add_argument("--svc-reps", type=int, default=5, help="timed service regions of K steps (median reported; 5: robust to two host hiccups)")
     ap.add_argument("--launch-only", action="store_true",
                     help="measure the launch path only (ranks sharing one GPU cannot each hold a service grid)")
     ap.add_argument("--window", type=int, default=256, help="br-host: header bytes per frame moved over PCIe")

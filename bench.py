@@ -58,6 +58,7 @@ writes the rewritten windows back.
 checks the launcher alone: N gloo ranks on the CPU, no GPU work, the line reports n_gpus.
 """
 import argparse
+import gc
 import json
 import os
 import socket
@@ -201,6 +202,9 @@ class World:
         end of its closing device synchronize; the closing barrier comes after the clock stops
         (with RCCL it is itself a collective launch and synchronize, tens of microseconds that are
         no part of any rank's K steps), and the max over ranks is the job's time."""
+        gc_on = gc.isenabled()
+        gc.collect()     # no garbage-collector pass inside the region (a host pause of its own)
+        gc.disable()
         self.barrier()
         self.sync()
         t0 = time.perf_counter()
@@ -208,6 +212,8 @@ class World:
             fn()
         self.sync()
         el = time.perf_counter() - t0
+        if gc_on:
+            gc.enable()
         self.barrier()
         all_el = self.gather(el)
         return max(all_el), all_el

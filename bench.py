@@ -202,8 +202,10 @@ class World:
         end of its closing device synchronize; the closing barrier comes after the clock stops
         (with RCCL it is itself a collective launch and synchronize, tens of microseconds that are
         no part of any rank's K steps), and the max over ranks is the job's time."""
+        # no garbage-collector pass inside the region (a host pause of its own); no collect()
+        # before it either: walking every object leaves the host caches cold, and the region's
+        # launch call then took 34-62 us instead of 9-13 (profiles/r03/drv3_gc_collect/)
         gc_on = gc.isenabled()
-        gc.collect()     # no garbage-collector pass inside the region (a host pause of its own)
         gc.disable()
         self.barrier()
         self.sync()

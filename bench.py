@@ -379,6 +379,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     W.sync()
     svc = {}
     posts = ctx.service_batches([(batches[k % R], n, bitmaps[k % nb]) for k in range(steps)])
+    run_posts = ctx.service_run_async_fn(posts)
 
     # hfv_service_run_async: the region's closing device synchronize is the only wait (the
     # waiting hfv_service_run, HFV_BENCH_ASYNC=0, spins on the grid's stream first: ~5 % slower,
@@ -388,7 +389,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
     def service_run():
         t = time.perf_counter()
         if run_async:   # the region's closing device synchronize waits for the grid
-            ctx.service_run_async(posts)
+            run_posts()
         else:
             svc["grid_ms"] = service_grid(ctx, batches, steps, bitmaps, n, posts)
         svc["call_us"] = (time.perf_counter() - t) * 1e6

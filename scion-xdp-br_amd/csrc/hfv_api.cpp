@@ -1593,6 +1593,17 @@ static void svc_balance(hfv_ctx *ctx)
     }
     if (span < 5000) return;   // 100 MHz ticks: 50 us
     const double mean = rsum / (double)G;
+    // A grid some of whose blocks ran far below the others was disturbed from outside (a
+    // transient on the box: blocks' rates normally stay within a few % of each other); learning
+    // from it would carry the disturbance into the next grids' shares.
+    double rmin = 1e300, rmax = 0;
+    for (uint64_t k = 0; k < G; ++k) {
+        const uint64_t a = ctx->svc_host->blk_start[k], b = ctx->svc_host->blk_fin[k];
+        const double r = tiles[k] / (double)(b - a);
+        rmin = r < rmin ? r : rmin;
+        rmax = r > rmax ? r : rmax;
+    }
+    if (rmax > 1.6 * rmin) return;
     auto blend = [&](uint32_t old, double rate) {
         double w = 0.5 * old + 0.5 * kSvcWeightUnit * rate / mean;
         if (w < kSvcWeightUnit / 2) w = kSvcWeightUnit / 2;

@@ -526,6 +526,21 @@ class Ctx:
         _check(lib().hfv_service_run_async(self._h, arr, len(arr), ctypes.byref(t)))
         return list(range(t.value, t.value + len(arr)))
 
+    def service_run_async_fn(self, batches):
+        """service_run_async as a prepared zero-argument call (the C function, the ctx handle, the
+        batch array and the ticket out-parameter bound once): what a timed loop calls, so that
+        the Python side of each call is one foreign-function call and a return-code check."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        f = lib().hfv_service_run_async
+        h, n, t = self._h, len(arr), ctypes.c_uint64()
+        tp = ctypes.byref(t)
+
+        def run():
+            rc = f(h, arr, n, tp)
+            if rc:
+                _check(rc)
+        return run
+
     def service_poll(self, ticket):
         rc = lib().hfv_service_poll(self._h, ticket)
         if rc < 0:

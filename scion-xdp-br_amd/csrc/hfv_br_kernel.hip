@@ -473,8 +473,9 @@ __device__ __forceinline__ DstKey dst_key(const BrFrame &k)
 
 __device__ __forceinline__ bool ingress_match(const DevBrIngress &e, const DstKey &d, uint32_t ifindex)
 {
-    return e.v4 == d.v4 && e.v6[0] == d.v6[0] && e.v6[1] == d.v6[1] && e.v6[2] == d.v6[2] && e.v6[3] == d.v6[3] &&
-           e.port == d.port && e.ifindex16 == (ifindex & 0xffffu);
+    // bitwise, not short-circuit: seven compares of LDS words, no branch (and exec mask) per field
+    return (e.v4 == d.v4) & (e.v6[0] == d.v6[0]) & (e.v6[1] == d.v6[1]) & (e.v6[2] == d.v6[2]) & (e.v6[3] == d.v6[3]) &
+           (e.port == d.port) & (e.ifindex16 == (ifindex & 0xffffu));
 }
 
 __device__ __forceinline__ int ingress_lookup(const BrFrame &k)

@@ -414,7 +414,8 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
             el, per_rank = W.timed(1, service_run)
             if run_async:
                 svc["grid_ms"] = ctx.service_stop()   # reaps the exited grid: its lifetime (0 untimed)
-            rs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"]))   # diagnostics
+            rs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"],
+                       ctx.service_weights()))   # diagnostics
             check(steps)
         return rs
 
@@ -425,13 +426,17 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         runs = truns
     runs.sort(key=lambda r: r[0])
     truns_s = sorted(truns, key=lambda r: r[2])
-    svc_el, per_rank, _, mhz, _ = runs[len(runs) // 2]
+    svc_el, per_rank, _, mhz, _, _ = runs[len(runs) // 2]
     grid_ms = truns_s[len(truns_s) // 2][2]
     out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
                 "svc_all_ms": [round(r[0] * 1e3, 4) for r in runs],
                 "svc_all_call_us": [round(r[4], 1) for r in runs],
                 "svc_timed_regions_ms": [round(r[0] * 1e3, 4) for r in truns],
                 "svc_all_grid_ms": [round(r[2], 4) for r in truns],
+                # per event-timed grid: its shader clock and the block weights it left for the
+                # next grid (a slow grid at a normal clock with skewed weights is a balance fault)
+                "svc_grid_mhz": [round(r[3], 1) if r[3] else None for r in truns],
+                "svc_weights": [r[5] for r in truns],
                 "svc_value_regions": "timed with dispatch events" if timed_value else "no timing events"})
     return out
 
@@ -916,6 +921,7 @@ def run_hf(args, W):
             "timed_regions_ms": m.get("svc_all_ms"), "grids_ms": m.get("svc_all_grid_ms"),
             "event_timed_regions_ms": m.get("svc_timed_regions_ms"), "value_regions": m.get("svc_value_regions"),
             "service_run_call_us": m.get("svc_all_call_us"),
+            "grids_mhz": m.get("svc_grid_mhz"), "weights": m.get("svc_weights"),
             "note": f"value = the median of {args.svc_reps} timed regions of K steps each (each a fresh grid)"},
         "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),
                        "ms_per_step": round(m["launch_el"] / args.steps * 1e3, 5),
@@ -988,6 +994,7 @@ def run_hf(args, W):
                              "mpkts": round(total * args.steps / m3["svc_el"] / 1e6, 2),
                              "ms_per_step": round(m3["svc_el"] / args.steps * 1e3, 5),
                              "grid_ms": round(m3["grid_ms"], 4), "frac": round(a3 / HBM_PEAK_GBS, 4),
+                             "grids_ms": m3["svc_all_grid_ms"], "grids_mhz": m3["svc_grid_mhz"],
                              "per_launch_mpkts": round(total * args.steps / m3["launch_el"] / 1e6, 2),
                              "shader_mhz": round(m3["mhz"], 1) if m3["mhz"] else None,
                              "ceilings": ceilings("ifid", n, m3["mhz"], cus)}

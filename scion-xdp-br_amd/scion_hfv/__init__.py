@@ -567,6 +567,16 @@ class Ctx:
         t0, r0, t1, r1 = (int(x) for x in clk[SVC_RING:SVC_RING + 4])
         return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
 
+    def service_weights(self):
+        """Diagnostic: the block weights the next service grid will use (per XCD 0..7, then
+        block 0's), in 1/1024 of an equal share (svc_balance, hfv_api.cpp)."""
+        w = (ctypes.c_uint32 * 9)()
+        L = lib()
+        L.hfv_debug_service_weights.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        if L.hfv_debug_service_weights(self._h, w) != 0:
+            return None
+        return [int(x) for x in w]
+
     def service_timeline(self, nbatches):
         """Diagnostic: per batch of the last grid, (relay published, block 0 loaded) in us
         after block 0's loop start, and the grid's loop span."""

@@ -222,6 +222,33 @@ def test_service_run_async(ctx, count):
     assert ctx.service_stop() > 0 and not ctx.service_running
 
 
+def test_service_balance_weights_stay_bounded(ctx):
+    """svc_balance (hfv_api.cpp) re-derives the per-XCD block weights after every run grid:
+    over a dozen K = 20 grids of 2^20 records (the bench's shape) they stay inside the clamp
+    [1/2, 2] of an equal share, and every grid's verdicts stay equal
+    to the launch path's whatever the shares."""
+    ctx.key_add(0, orc.KEY_1111)
+    n = 1 << 20
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=DEV)
+    ctx.gen_records(recs, n, orc.SEED_RECORDS)
+    want = new_bits(n)
+    ctx.verify_records(recs, n, want)
+    outs = [new_bits(n, fill=-1) for _ in range(20)]
+    torch.cuda.synchronize()
+    for _ in range(12):
+        for o in outs:
+            o.fill_(-1)
+        torch.cuda.synchronize()
+        ctx.service_run_async([(recs, n, o) for o in outs])
+        torch.cuda.synchronize()
+        assert ctx.service_stop() >= 0
+        for o in outs:
+            assert torch.equal(o, want)
+        w = ctx.service_weights()
+        assert w is not None and len(w) == 9
+        assert all(512 <= x <= 2048 for x in w), w   # (quiet boxes: within -10 % / +5 %, profiles/r03/slowgrid/)
+
+
 @pytest.mark.parametrize("then", ["submit", "submitv", "start_submit"])
 def test_service_submit_after_run_async(ctx, then):
     """after hfv_service_run_async the grid exits on its own stop; a later

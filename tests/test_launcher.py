@@ -59,3 +59,25 @@ def test_two_service_ranks_on_one_gpu():
     assert d["roofline"]["kernel"] == "k_verify_service" and d["value"] > 0
     assert int(d["same_device"]["service_grid_blocks"]) * 2 <= 256
     assert d["host_threads"]["ranks_on_node"] == 2 and d["host_threads"]["budget"] >= 1   # OMP_NUM_THREADS=1 here
+
+
+@pytest.mark.gpu
+def test_single_rank_line_keeps_the_contract():
+    """The driver's N = 1 line: every contract key, `value` = whole-job Mpkt/s over the timed
+    steps, the roofline and cpu_baseline objects (bench contract, task 4), and the per-grid
+    clock and balance-weight diagnostics of the service regions."""
+    d = _bench("--steps", "6", "--warmup", "2", "--no-extras", "--no-host-e2e", "--loop-n", "0", "--cpu-budget", "1",
+               timeout=600)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 6 and d["warmup"] == 2 and d["higher_is_better"] is True
+    assert d["unit"] == "Mpkt/s" and d["dtype"] == "u8" and "workload" in d["config"]
+    assert abs(d["value"] - 2 ** 20 / (d["ms_per_step"] * 1e-3) / 1e6) / d["value"] < 0.01
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    c = d["cpu_baseline"]
+    assert c["value"] > 0 and c["cores"] >= 1 and c["kind"] in ("reference", "port") and c["sample"]
+    s = d["service"]
+    assert len(s["grids_mhz"]) == len(s["grids_ms"]) and all(len(w) == 9 for w in s["weights"])

@@ -708,12 +708,15 @@ int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
 {
     if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");
     const KernelVariant &a = ctx->geom.single, &b = ctx->geom.multi;
+    // the resident service's per-interface key layout (launch_service, hfv_kernels.hip)
+    const char *iv = getenv("HFV_SVC_IFID");
+    const char *svc_ifid = iv && !strcmp(iv, "gather") ? "gather" : iv && !strcmp(iv, "lds") ? "lds" : "sched";
     snprintf(buf, len,
              "zero: block=%d pf=%d tab=%d dma=%d np=%d dyn=%d bs=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d dma=%d "
-             "np=%d dyn=%d grid=%dx%d",
+             "np=%d dyn=%d grid=%dx%d; service ifid keys=%s tab=%d",
              a.block, a.pf, a.tab, a.dma, a.np, a.dyn, a.bs, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab,
              b.dma,
-             b.np, b.dyn, ctx->geom.num_cus, b.blocks_per_cu);
+             b.np, b.dyn, ctx->geom.num_cus, b.blocks_per_cu, svc_ifid, strcmp(svc_ifid, "lds") ? 4 : 2);
     return 0;
 }
 

@@ -234,7 +234,7 @@ struct hfv_ctx {
     hipStream_t svc_stream = nullptr;
     SvcShared *svc_host = nullptr;   // descriptor ring + completions, coherent pinned memory
     SvcShared *svc_host_dev = nullptr;
-    SvcDesc *svc_mirror = nullptr;   // device copy of the descriptor ring (the grid's relay writes it)
+    SvcDev *svc_dev = nullptr;       // device side: relayed descriptors, block completions, diagnostics
     unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
     uint64_t svc_next = 1;           // next grid-local batch number (1, 2, ... per grid)
     uint64_t svc_base = 1;           // ticket of the running grid's batch 1 (tickets are monotonic per ctx)
@@ -465,7 +465,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         (void)hipStreamDestroy(ctx->svc_stream);
     }
     if (ctx->svc_host) (void)hipHostFree(ctx->svc_host);
-    if (ctx->svc_mirror) (void)hipFree(ctx->svc_mirror);
+    if (ctx->svc_dev) (void)hipFree(ctx->svc_dev);
     for (int i = 0; i < 2; ++i)
         if (ctx->svc_ev[i]) (void)hipEventDestroy(ctx->svc_ev[i]);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -1499,13 +1499,41 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
 
 }  // extern "C"
 
-// Grid-local batch t is complete when every block of the grid has reported its share of it.
+// Grid-local batch t is complete once the relay has forwarded its completion (every block of
+// the grid reported its share of it).
 static bool svc_is_done(const hfv_ctx *ctx, uint64_t t)
 {
-    const uint64_t *d = ctx->svc_host->done[(t - 1) % kSvcRing];
+    return __atomic_load_n(&ctx->svc_host->done[(t - 1) % kSvcRing], __ATOMIC_ACQUIRE) >= (ctx->svc_tag | t);
+}
+
+// The running grid has exited on the stop the host posted: it verified every batch before it
+// (each block reaches the stop only after its share of all earlier batches), including those
+// whose completion the relay did not forward (it leaves at the stop).
+static bool svc_exited_clean(const hfv_ctx *ctx)
+{
+    return ctx->svc_running && ctx->svc_stop_posted && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0 &&
+           hipStreamQuery(ctx->svc_stream) == hipSuccess;
+}
+
+// Device-side completion of grid-local batch t from a copy of SvcDev::done (after an idle or
+// watchdog exit, when the relay may not have forwarded everything).
+static bool svc_dev_done(const hfv_ctx *ctx, const std::vector<uint64_t> &done, uint64_t t)
+{
+    const uint64_t *d = &done[((t - 1) % kSvcRing) * kSvcMaxBlocks];
     for (unsigned k = 0; k < ctx->svc_grid; ++k)
-        if (__atomic_load_n(&d[k], __ATOMIC_ACQUIRE) < (ctx->svc_tag | t)) return false;
+        if (d[k] < (ctx->svc_tag | t)) return false;
     return true;
+}
+
+// Copy `bytes` at byte offset `off` of the ctx's SvcDev to host memory (diagnostics and the
+// balance, after a grid; on the ctx's own stream, which a running grid does not occupy).
+static int svc_dev_read(hfv_ctx *ctx, void *dst, size_t off, size_t bytes)
+{
+    if (!ctx->svc_dev) return fail(-EINVAL, "the verify service has not run");
+    HIP_TRY(hipMemcpyAsync(dst, reinterpret_cast<const char *>(ctx->svc_dev) + off, bytes, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
 }
 
 static int svc_wait_done(hfv_ctx *ctx, uint64_t t, int timeout_ms)
@@ -1518,13 +1546,17 @@ static int svc_wait_done(hfv_ctx *ctx, uint64_t t, int timeout_ms)
             __builtin_ia32_pause();
             continue;
         }
-        if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0)
+        if (hipStreamQuery(ctx->svc_stream) == hipSuccess) {   // the grid is gone
+            if (svc_exited_clean(ctx)) return 0;
+            std::vector<uint64_t> done((size_t)kSvcRing * kSvcMaxBlocks);
+            int rc = svc_dev_read(ctx, done.data(), offsetof(SvcDev, done), done.size() * 8);
+            if (rc) return rc;
+            if (svc_dev_done(ctx, done, t)) return 0;
+            const uint64_t st = __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE);
             return fail(-EIO, "verify service exited (%s); ticket %llu will not complete",
-                        ctx->svc_host->status == kSvcIdleTimeout ? "idle timeout" : "watchdog",
+                        st == kSvcIdleTimeout ? "idle timeout" : st == kSvcWatchdog ? "watchdog" : "grid ended",
                         (unsigned long long)(ctx->svc_base + t - 1));
-        if (hipStreamQuery(ctx->svc_stream) == hipSuccess)
-            return fail(-EIO, "verify service grid has exited; ticket %llu will not complete",
-                        (unsigned long long)(ctx->svc_base + t - 1));
+        }
         clock_gettime(CLOCK_MONOTONIC, &now);
         double ms = (now.tv_sec - t0.tv_sec) * 1e3 + (now.tv_nsec - t0.tv_nsec) * 1e-6;
         if (timeout_ms >= 0 && ms > timeout_ms)
@@ -1565,6 +1597,10 @@ static void svc_balance(hfv_ctx *ctx)
     static const bool off = getenv("HFV_SVC_BALANCE") && !strcmp(getenv("HFV_SVC_BALANCE"), "0");
     const uint64_t G = ctx->svc_grid;
     if (off || G < 16 || ctx->svc_run_ns.empty()) return;
+    std::vector<uint64_t> bt(2 * kSvcMaxBlocks);   // blk_start[], blk_fin[] (adjacent in SvcDev)
+    static_assert(offsetof(SvcDev, blk_fin) == offsetof(SvcDev, blk_start) + kSvcMaxBlocks * 8, "layout");
+    if (svc_dev_read(ctx, bt.data(), offsetof(SvcDev, blk_start), bt.size() * 8)) return;
+    const uint64_t *blk_start = bt.data(), *blk_fin = bt.data() + kSvcMaxBlocks;
     const SvcWeights &wu = ctx->svc_w_used;
     std::vector<uint64_t> cum(G + 1, 0);
     for (uint64_t k = 0; k < G; ++k) cum[k + 1] = cum[k] + (k ? wu.w[k % 8] : wu.w0);
@@ -1582,8 +1618,7 @@ static void svc_balance(hfv_ctx *ctx)
     int cx[8] = {0};
     uint64_t span = 0;
     for (uint64_t k = 0; k < G; ++k) {
-        const uint64_t a = __atomic_load_n(&ctx->svc_host->blk_start[k], __ATOMIC_ACQUIRE);
-        const uint64_t b = __atomic_load_n(&ctx->svc_host->blk_fin[k], __ATOMIC_ACQUIRE);
+        const uint64_t a = blk_start[k], b = blk_fin[k];
         if (b <= a || tiles[k] <= 0) return;   // a block without a measurement: keep the weights
         if (b - a > span) span = b - a;
         const double r = tiles[k] / (double)(b - a);
@@ -1601,7 +1636,7 @@ static void svc_balance(hfv_ctx *ctx)
     // from it would carry the disturbance into the next grids' shares.
     double rmin = 1e300, rmax = 0;
     for (uint64_t k = 0; k < G; ++k) {
-        const uint64_t a = ctx->svc_host->blk_start[k], b = ctx->svc_host->blk_fin[k];
+        const uint64_t a = blk_start[k], b = blk_fin[k];
         const double r = tiles[k] / (double)(b - a);
         rmin = r < rmin ? r : rmin;
         rmax = r > rmax ? r : rmax;
@@ -1653,12 +1688,15 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     // A grid that left on the stop descriptor verified every batch before it (each block
     // reaches the stop only after its share of all earlier batches).  An idle or watchdog
     // exit is clean unless it left a posted batch unverified (batches may complete out of
-    // order; only the newest kSvcRing can still be open): scan those.  (The scan reads
-    // kSvcRing x grid completion words, ~0.1 ms; it is not paid on a normal stop.)
+    // order; only the newest kSvcRing can still be open): scan those in a copy of the device
+    // completion words (the relay may have left before forwarding them; not paid on a normal stop).
     if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) return 0;
+    std::vector<uint64_t> done((size_t)kSvcRing * kSvcMaxBlocks);
+    rc = svc_dev_read(ctx, done.data(), offsetof(SvcDev, done), done.size() * 8);
+    if (rc) return rc;
     uint64_t first_lost = 0;
     for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t)
-        if (!svc_is_done(ctx, t)) {
+        if (!svc_dev_done(ctx, done, t)) {
             first_lost = ctx->svc_base + t - 1;
             if (ctx->svc_lost.size() >= 4096) ctx->svc_lost.erase(ctx->svc_lost.begin(), ctx->svc_lost.begin() + 1024);
             ctx->svc_lost.push_back(first_lost);
@@ -1670,17 +1708,16 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
 }
 
 // Ticket state: 1 done, 0 pending, -EIO lost (its grid stopped without verifying it),
-// -EINVAL never issued.  Tickets below the running grid's base belong to stopped grids,
-// which verified every batch posted to them unless they exited on a timeout (svc_lost).
+// -EINVAL never issued.  Tickets of stopped grids were verified unless they exited on a
+// timeout (svc_lost); tickets of the running grid are done once their completion was
+// forwarded, or once the grid has left on its stop.
 static int svc_ticket_state(const hfv_ctx *ctx, uint64_t ticket)
 {
     if (!ctx->svc_host || ticket == 0 || ticket >= ctx->svc_ticket) return -EINVAL;
-    if (ticket < ctx->svc_base || !ctx->svc_running) {
-        for (uint64_t l : ctx->svc_lost)
-            if (l == ticket) return -EIO;
-        if (ticket < ctx->svc_base) return 1;
-    }
-    return svc_is_done(ctx, ticket - ctx->svc_base + 1) ? 1 : 0;
+    for (uint64_t l : ctx->svc_lost)
+        if (l == ticket) return -EIO;
+    if (ticket < ctx->svc_base || !ctx->svc_running) return 1;
+    return svc_is_done(ctx, ticket - ctx->svc_base + 1) || svc_exited_clean(ctx) ? 1 : 0;
 }
 
 static int svc_quiesce(hfv_ctx *ctx) { return ctx->svc_running ? svc_stop(ctx, nullptr) : 0; }
@@ -1702,15 +1739,17 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
         HIP_TRY(hipHostMalloc((void **)&ctx->svc_host, sizeof(SvcShared),
                               hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&ctx->svc_host_dev, ctx->svc_host, 0));
-        HIP_TRY(hipMalloc((void **)&ctx->svc_mirror, kSvcRing * sizeof(SvcDesc)));
+        HIP_TRY(hipMalloc((void **)&ctx->svc_dev, sizeof(SvcDev)));
         for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreate(&ctx->svc_ev[i]));
         memset(ctx->svc_host, 0, sizeof(SvcShared));
-        HIP_TRY(hipMemsetAsync(ctx->svc_mirror, 0, kSvcRing * sizeof(SvcDesc), ctx->svc_stream));
+        HIP_TRY(hipMemsetAsync(ctx->svc_dev, 0, sizeof(SvcDev), ctx->svc_stream));
     }
     // a new generation: words an earlier grid left in the ring, the mirror and the completion
-    // table carry a smaller tag and never match
+    // tables carry a smaller tag and never match
     ctx->svc_tag += 1ull << 40;
     __atomic_store_n(&ctx->svc_host->status, 0, __ATOMIC_RELEASE);
+    // the relay's counters are per grid (zeroed in stream order before the launch)
+    HIP_TRY(hipMemsetAsync(&ctx->svc_dev->relay[0], 0, sizeof(ctx->svc_dev->relay), ctx->svc_stream));
     int rc = publish_keys(ctx, ctx->svc_stream, ds);
     if (rc) return rc;
     ctx->svc_keysel = ctx->keysel;
@@ -1724,22 +1763,36 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
     return 0;
 }
 
+static uint32_t g_svc_relay_delay_us = 0;   // hfv_debug_relay_delay
+
 static int svc_launch(hfv_ctx *ctx, DevState *ds)
 {
     const bool noev = !ctx->svc_timing;
     ctx->svc_timed = !noev;
-    // batch 0 of this grid, if the caller posted it before the launch (svc_run, submitv): in the
-    // kernel arguments as well, so the blocks need not wait for the relay to fetch it
-    SvcFirst first = {0, 0, 0, 0};
-    if (ctx->svc_next > 1) {
-        const SvcDesc &d = ctx->svc_host->desc[0];
-        first = {d.recs, d.bits, d.n, d.n == kSvcStopN ? 1u : d.stride};
-    }
+    // the batches (and the stop) the caller posted before the launch (svc_run, submitv): the
+    // first kSvcInline travel in the kernel arguments, so the blocks start on them without any
+    // host round trip; the relay fetches the rest
+    SvcArgs a;
+    memset(&a, 0, sizeof a);
+    a.tab = &ds->keys;
+    a.ttab_img = ctx->geom.ttab_img;
+    a.host = ctx->svc_host_dev;
+    a.dev = ctx->svc_dev;
+    a.inf_off = ctx->inf_off;
+    a.hf_off = ctx->hf_off;
+    a.idle_ticks = (uint64_t)ctx->svc_idle_ms * 100000ull;
+    a.tag = ctx->svc_tag;
     ctx->svc_w_used = ctx->svc_w;
-    int e = launch_verify_service(ctx->geom, &ds->keys, ctx->keysel, ctx->svc_host_dev, ctx->svc_mirror, ctx->inf_off,
-                                  ctx->hf_off, (uint64_t)ctx->svc_idle_ms * 100000ull, ctx->svc_tag, first,
-                                  ctx->svc_w_used, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0], noev ? nullptr : ctx->svc_ev[1],
-                                  &ctx->svc_grid);
+    a.weights = ctx->svc_w_used;
+    const uint64_t posted = ctx->svc_next - 1;
+    a.n_inline = (uint32_t)(posted < kSvcInline ? posted : kSvcInline);
+    for (uint32_t i = 0; i < a.n_inline; ++i) {
+        const SvcDesc &d = ctx->svc_host->desc[i];
+        a.inl[i] = {d.recs, d.bits, d.n, d.stride};
+    }
+    a.relay_delay_us = g_svc_relay_delay_us;
+    int e = launch_verify_service(ctx->geom, ctx->keysel, a, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0],
+                                  noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ctx->svc_running = true;
@@ -1981,28 +2034,45 @@ int hfv_debug_service_weights(hfv_ctx *ctx, uint32_t out[9])
 // 16 words, block * 16 + wave; 0 for a wave that did not run the loop), s_memrealtime (100 MHz).
 int hfv_debug_service_span(hfv_ctx *ctx, uint64_t *out, size_t words)
 {
-    if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
+    if (!ctx || !out || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
     const size_t g = ctx->svc_grid;
     if (words < g * 18) return fail(-EINVAL, "need %zu words", g * 18);
-    for (size_t i = 0; i < g; ++i) {
-        out[i] = __atomic_load_n(&ctx->svc_host->span_entry[i], __ATOMIC_ACQUIRE);
-        out[g + i] = __atomic_load_n(&ctx->svc_host->span_fill[i], __ATOMIC_ACQUIRE);
-    }
-    for (size_t i = 0; i < g * 16; ++i) out[2 * g + i] = __atomic_load_n(&ctx->svc_host->span_exit[i], __ATOMIC_ACQUIRE);
-    return 0;
+    int rc = svc_dev_read(ctx, out, offsetof(SvcDev, span_entry), g * 8);
+    if (!rc) rc = svc_dev_read(ctx, out + g, offsetof(SvcDev, span_fill), g * 8);
+    if (!rc) rc = svc_dev_read(ctx, out + 2 * g, offsetof(SvcDev, span_exit), g * 16 * 8);
+    return rc;
 }
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
-// 0 loaded ring slot i's descriptor (i < kSvcRing); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and
-// s_memrealtime at its start and at its exit (the shader clock over the grid's life);
-// out[kSvcRing + 4 + i] = s_memrealtime when the relay published slot i (2 * kSvcRing + 4 words).
+// 0 loaded ring slot i's descriptor from the mirror (i < kSvcRing; inline batches are not
+// loaded); out[kSvcRing .. kSvcRing + 3] = block 0 wave 0's s_memtime and s_memrealtime at its
+// start and at its exit (the shader clock over the grid's life); out[kSvcRing + 4 + i] =
+// s_memrealtime when the relay published slot i (2 * kSvcRing + 4 words).
 int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
 {
-    if (!ctx || !out || !ctx->svc_host) return fail(-EINVAL, "bad argument");
-    for (uint32_t i = 0; i < kSvcRing; ++i) out[i] = __atomic_load_n(&ctx->svc_host->load_clock[i], __ATOMIC_ACQUIRE);
-    for (uint32_t i = 0; i < 4; ++i) out[kSvcRing + i] = __atomic_load_n(&ctx->svc_host->run_clock[i], __ATOMIC_ACQUIRE);
-    for (uint32_t i = 0; i < kSvcRing; ++i)
-        out[kSvcRing + 4 + i] = __atomic_load_n(&ctx->svc_host->relay_clock[i], __ATOMIC_ACQUIRE);
+    if (!ctx || !out || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
+    static_assert(offsetof(SvcDev, relay) == offsetof(SvcDev, run_clock) + 32, "layout");
+    int rc = svc_dev_read(ctx, out, offsetof(SvcDev, load_clock), kSvcRing * 8);
+    if (!rc) rc = svc_dev_read(ctx, out + kSvcRing, offsetof(SvcDev, run_clock), 4 * 8);
+    if (!rc) rc = svc_dev_read(ctx, out + kSvcRing + 4, offsetof(SvcDev, relay_clock), kSvcRing * 8);
+    return rc;
+}
+
+// Diagnostic (not part of include/scion_hfv.h): the last grid's relay counters (SvcRelayStat,
+// 8 words): the host round trip probed at grid start, host reads and their summed / longest
+// round trips (100 MHz ticks), descriptors relayed, completions forwarded, waits of a block for
+// a descriptor, descriptors in the kernel arguments.
+int hfv_debug_service_relay(hfv_ctx *ctx, uint64_t out[8])
+{
+    if (!ctx || !out || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
+    return svc_dev_read(ctx, out, offsetof(SvcDev, relay), 8 * 8);
+}
+
+// Test hook (not part of include/scion_hfv.h): every host read of later service grids' relay
+// wave takes `us` microseconds longer (a slow PCIe link), 0 = off.
+int hfv_debug_relay_delay(uint32_t us)
+{
+    g_svc_relay_delay_us = us > 100000u ? 100000u : us;
     return 0;
 }
 

@@ -95,40 +95,64 @@ void compile_br_config(const hfv_br_config *in, DevBrConfig *out);
 
 enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 
-// Resident verify service (hfv_service_*): the host posts batch descriptors into a ring in
-// pinned, coherent host memory; one wave of the persistent grid copies each posted
-// descriptor into a device-memory mirror (SvcDesc[kSvcRing]) that every block polls instead
-// of reaching over PCIe; the grid verifies each batch, and every
-// block publishes the completion of its share of a batch straight into host memory (one
-// posted PCIe write; the host combines the per-block flags).  Batch b (0-based, ticket b+1)
-// uses ring slot b % kSvcRing; the host posts ticket t only once ticket t - kSvcRing is
-// complete, which is what lets each block cache kSvcRing descriptors in LDS without any
-// reuse check (hfv_kernels.hip, k_verify_service).
+// Resident verify service (hfv_service_*).  The host posts batch descriptors into a ring in
+// pinned, coherent host memory (SvcShared).  Batches posted before the grid starts (every
+// hfv_service_run / run_async batch up to kSvcInline, and submitv's first ones) travel in the
+// kernel arguments (SvcArgs::inl) and every block caches them in LDS at its start: no PCIe
+// round trip stands between the grid and those batches.  Batches posted later are fetched by
+// one relay wave of block 0, up to 64 descriptors per host read (read-ahead), into a device
+// mirror (SvcDev::mir) that the blocks poll.  Blocks report the completion of their share of
+// a batch into device memory (SvcDev::done); the relay forwards a batch's completion to the
+// host ring (SvcShared::done) once every block has reported it.  So the compute waves never
+// touch host memory, and no wave waits on a PCIe round trip per batch (round 3's relay did a
+// seq poll, a field read and a host store per batch on the blocks' critical path: ~42 us per
+// batch on a box whose host round trips were slow).  Batch b (0-based, ticket
+// b+1) uses ring slot b % kSvcRing; the host posts ticket t only once ticket t - kSvcRing is
+// complete, which is what lets each block cache kSvcRing descriptors in LDS without any reuse
+// check (hfv_kernels.hip, k_verify_service).  A grid that exits on its stop descriptor has
+// verified every batch before it, so the host needs no forwarded completion for those.
 constexpr uint32_t kSvcRing = 256;   // batches in flight (a host hiccup of ~3 ms at 2^20 records does not starve the grid)
 constexpr uint32_t kSvcMaxBlocks = 1024;
+constexpr uint32_t kSvcInline = 64;  // descriptors in the kernel arguments
 constexpr uint64_t kSvcStopN = ~0ull;   // descriptor n: the service exits
 struct SvcDesc {
     uint64_t recs, bits, n, stride;   // device pointers / counts of the batch
     uint64_t seq;                     // generation tag | ticket; stored last, with release
     uint64_t pad[3];
 };
-struct SvcShared {
+struct SvcShared {   // pinned host memory
     SvcDesc desc[kSvcRing];
     uint64_t status;                 // nonzero: the grid stopped on its own (kSvcIdleTimeout, kSvcWatchdog)
     uint64_t pad[7];
-    uint64_t load_clock[kSvcRing];   // diagnostics: s_memrealtime when block 0 loaded the slot
-    uint64_t run_clock[4];           // diagnostics: block 0 wave 0 s_memtime/s_memrealtime at start, at exit
-    uint64_t relay_clock[kSvcRing];  // diagnostics: s_memrealtime when the relay published the slot
+    uint64_t done[kSvcRing];         // done[(t-1) % kSvcRing] = tag | t: batch t verified (forwarded by the relay)
     uint64_t prof[8];                // diagnostics (HFV_SVC_PROF builds): shader cycles per loop phase, summed over waves
-    // diagnostics (HFV_SVC_SPAN builds): s_memrealtime at each block's entry and after its table
-    // fill, and at each wave's exit (block * 16 + wave)
-    uint64_t span_entry[kSvcMaxBlocks];
-    uint64_t span_fill[kSvcMaxBlocks];
-    uint64_t span_exit[kSvcMaxBlocks * 16];
+};
+// Relay diagnostics (SvcDev::relay), one grid's worth: how the host link behaved for it.
+enum SvcRelayStat {
+    kRelayProbeTicks = 0,   // one host-memory read round trip at grid start (100 MHz ticks)
+    kRelayReads = 1,        // host ring reads (each covers up to 64 descriptors)
+    kRelayReadTicks = 2,    // ... their summed round trips
+    kRelayReadMax = 3,      // ... the longest
+    kRelayDescs = 4,        // descriptors relayed (batches beyond the inline ones)
+    kRelayForwarded = 5,    // batch completions forwarded to the host
+    kRelayBlockWaits = 6,   // times a wave waited for a descriptor the relay had not published
+    kRelayInline = 7,       // descriptors the grid got in its kernel arguments
+};
+struct SvcDev {   // device memory: written by the grid; the host copies what it needs after it
+    SvcDesc mir[kSvcRing];           // relayed descriptors
+    uint64_t run_clock[4];           // block 0 wave 0 s_memtime/s_memrealtime at loop start, at exit
+    uint64_t relay[8];               // SvcRelayStat
+    uint64_t load_clock[kSvcRing];   // s_memrealtime when block 0 loaded the slot
+    uint64_t relay_clock[kSvcRing];  // s_memrealtime when the relay published the slot
     // work balance (SvcWeights): s_memrealtime when block k finished its table fill, and when it
     // last completed its share of a batch
     uint64_t blk_start[kSvcMaxBlocks];
     uint64_t blk_fin[kSvcMaxBlocks];
+    // HFV_SVC_SPAN builds: s_memrealtime at each block's entry and after its table fill, and at
+    // each wave's exit (block * 16 + wave)
+    uint64_t span_entry[kSvcMaxBlocks];
+    uint64_t span_fill[kSvcMaxBlocks];
+    uint64_t span_exit[kSvcMaxBlocks * 16];
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
@@ -179,9 +203,7 @@ int build_ttab_image(uint32_t *img, void *stream);
 // persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
 // block waits for the next descriptor before it exits with status kSvcIdleTimeout
 // returns the grid size in *grid
-// The first batch travels in the kernel arguments too (stride 0: none posted before launch), so
-// every block starts on it without waiting for the relay's PCIe round trips.
-struct SvcFirst {
+struct SvcDescLite {
     uint64_t recs, bits, n, stride;
 };
 // Work balance of the resident grid.  The XCDs of one MI355X do not verify at the same rate
@@ -207,10 +229,22 @@ constexpr uint64_t svc_cum(const SvcWeights &sw, uint64_t k)
     }
     return (k / 8) * all + part - sw.w[0] + sw.w0;
 }
-int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
-                          uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, SvcWeights weights,
-                          void *stream, void *ev_start, void *ev_stop, unsigned *grid);
+// Everything a service grid takes, passed as ONE kernel argument (so the kernel reads the
+// inline descriptors straight from the kernarg segment, indexed by batch).
+struct SvcArgs {
+    const DevKeyTable *tab;
+    const uint32_t *ttab_img;
+    SvcShared *host;   // device view of the pinned ring
+    SvcDev *dev;
+    uint32_t inf_off, hf_off;
+    uint64_t idle_ticks, tag;
+    SvcWeights weights;
+    uint32_t n_inline;        // descriptors in inl[] (batches 0 .. n_inline - 1; may end with a stop)
+    uint32_t relay_delay_us;  // test hook (hfv_debug_relay_delay): the relay spins this long after each host read
+    SvcDescLite inl[kSvcInline];
+};
+int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
+                          void *ev_stop, unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

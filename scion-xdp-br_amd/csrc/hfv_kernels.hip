@@ -662,8 +662,9 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
 //
 // Completion: verdict words are written through (system-scope stores); a wave counts its
 // verified tiles in the slot's LDS counter once those stores are acknowledged (vmcnt(0)),
-// and the wave that completes the block's share stores the ticket into host->done[slot][k]
-// (svc_complete); the host combines the per-block flags.
+// and the wave that completes the block's share stores the ticket into dev->done[slot][k]
+// (svc_complete, device memory); the relay wave forwards a batch's completion to the host
+// once every block has reported it.
 struct SvcSlot {
     uint32_t base, count;   // block tile numbers [base, base + count)
     uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
@@ -728,7 +729,7 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 #define HFV_SVC_PROF 0
 #endif
 // HFV_SVC_SPAN = 1: diagnostic build; block entry, table-fill and wave exit stamps
-// (s_memrealtime, 100 MHz) into host->span_* (hfv_debug_service_span)
+// (s_memrealtime, 100 MHz) into dev->span_* (hfv_debug_service_span)
 #ifndef HFV_SVC_SPAN
 #define HFV_SVC_SPAN 0
 #endif
@@ -775,67 +776,157 @@ struct SvcProf {
 };
 
 // This block's share of batch b is verified (one lane).  The verdict words were written
-// through to memory (system-scope stores) and every wave waited for its stores'
-// acknowledgement before counting its tiles, so nothing of the batch is left in L2: the
-// block reports straight to the host, no L2 writeback (buffer_wbl2 per block per batch
-// measured ~35 us per batch) and no grid-wide atomic (256 blocks on one counter serialise
-// at the memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/).
-__device__ void svc_complete(SvcShared *host, uint32_t b)
+// through to memory (system-scope stores) and every wave waited for their acknowledgement
+// before counting its tiles, so nothing of the batch is left in L2.  The completion word goes
+// to device memory (agent scope: written through to the memory side, where the relay wave of
+// block 0 reads it); no grid-wide atomic (256 blocks on one counter serialise at the
+// memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/) and no
+// host-memory store whose acknowledgement a compute wave would wait for.
+__device__ void svc_complete(SvcDev *dev, uint64_t tag, uint32_t b)
 {
-    __hip_atomic_store(&host->blk_fin[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&host->done[b % kSvcRing][blockIdx.x], s_svc_tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    dev->blk_fin[blockIdx.x] = __builtin_amdgcn_s_memrealtime();   // read by the host after the grid
+    __hip_atomic_store(&dev->done[b % kSvcRing][blockIdx.x], tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Descriptor relay (one lane of block 0's last wave, for the service's whole life): copy
-// each batch descriptor the host posts into the device-memory mirror `mir`, in ticket
-// order.  Every other block then reads its descriptors from device memory (coherent
-// agent-scope loads, served by the memory-side Infinity Cache) instead of from host memory
-// over PCIe: with 256 blocks each fetching every descriptor from the host, the per-batch
-// PCIe reads cost 25-35 us per batch (svc_probe: grid 32/128/256 -> 75/36/45 us per 2^20
-// batch against an 11 us compute bound).  The relay also owns the idle timeout: after
-// idle_ticks without a new host post it publishes a stop descriptor.
-__device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks, uint64_t tag)
+__device__ __forceinline__ uint64_t memrealtime() { return __builtin_amdgcn_s_memrealtime(); }
+
+// Test hook (hfv_debug_relay_delay): a host round trip `us` microseconds longer.
+__device__ __forceinline__ void relay_spin(uint32_t us)
 {
-    for (uint32_t b = 0;; ++b) {
-        const uint32_t slot = b % kSvcRing;
-        SvcDesc *h = &host->desc[slot];
-        bool idle = false;
-        const uint64_t want = tag | ((uint64_t)b + 1);
-        if (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
-                    idle = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        uint64_t recs = 0, bits = 0, n = kSvcStopN, stride = 0;
-        if (idle) {
-            __hip_atomic_store(&host->status, kSvcIdleTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // fields only after seq was seen
-            typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
-            const u64x4 f = __builtin_nontemporal_load(reinterpret_cast<const u64x4 *>(&h->recs));
-            recs = f.x;
-            bits = f.y;
-            n = f.z;
-            stride = f.w;
-        }
-        SvcDesc *m = &mir[slot];
-        // write-through (agent-scope) field stores, acknowledged before seq is published
-        __hip_atomic_store(&m->recs, recs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&m->bits, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&m->n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&m->stride, stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!us) return;
+    const uint64_t t0 = memrealtime();
+    while (memrealtime() - t0 < 100ull * us) __builtin_amdgcn_s_sleep(4);
+}
+
+// Descriptor relay and completion forwarder: block 0's last wave, all 64 lanes, for the grid's
+// life.  It fetches the descriptors the host posts after the inline ones (batches n_inline,
+// n_inline + 1, ...) into the device mirror `dev->mir`, in ticket order, up to 64 per host read:
+// lane 0 looks at the next slot's seq; once it is posted, every lane reads the seq of one of
+// the next 64 slots, the posted prefix's fields are read, copied (write-through agent-scope
+// stores) and their seqs published after the fields are acknowledged.  It also forwards batch
+// completions to the host ring (dev->done[slot][0..G) -> host->done[slot]), which the host
+// needs only while the grid runs (to reuse ring slots, and for hfv_service_poll/wait).  The
+// blocks never wait for this wave unless a batch's descriptor was posted after the grid
+// started and has not been fetched yet (kRelayBlockWaits).  It owns the idle timeout: after
+// idle_ticks without a new post it publishes a stop descriptor.  It leaves as soon as it has
+// published a stop: a grid that exits on its stop has verified everything before it, and the
+// host infers those completions from the grid's exit, so the relay never holds the grid open.
+__device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
+{
+    SvcShared *host = a.host;
+    SvcDev *dev = a.dev;
+    const uint64_t tag = a.tag;
+    const uint32_t n_in = a.n_inline;
+    bool stop = n_in && a.inl[n_in - 1].n == kSvcStopN;
+    uint32_t b = n_in;                       // next batch to relay
+    uint32_t stop_b = stop ? n_in - 1 : ~0u;
+    uint32_t f = 0;                          // next batch whose completion is forwarded
+    uint64_t reads = 0, rticks = 0, rmax = 0, descs = 0, fwd = 0;
+    auto timed_wait = [&]() {                // wait for this wave's host reads; account the trip
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&m->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&host->relay_clock[slot], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);   // diagnostics (a posted write)
-        if (n == kSvcStopN) return;
+    };
+    // one host-memory read at grid start: the PCIe round trip this grid saw (diagnostic)
+    uint64_t t0 = memrealtime();
+    uint64_t probe_v = __hip_atomic_load(&host->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    timed_wait();
+    const uint64_t probe = memrealtime() - t0 + (probe_v == 0x5eedull ? 1 : 0);
+    relay_spin(a.relay_delay_us);
+    uint64_t t_idle = memrealtime();
+    while (!stop) {
+        bool prog = false;
+        // is the next slot posted?
+        uint64_t s0 = 0;
+        t0 = memrealtime();
+        if (lane == 0) s0 = __hip_atomic_load(&host->desc[b % kSvcRing].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_wait();
+        uint64_t rt = memrealtime() - t0;
+        relay_spin(a.relay_delay_us);
+        ++reads;
+        rticks += rt;
+        rmax = rt > rmax ? rt : rmax;
+        if (wave_uniform64(s0) == (tag | ((uint64_t)b + 1))) {
+            // read ahead: the seqs of the next 64 slots, then the fields of the posted prefix
+            const uint32_t bi = b + lane;
+            const uint64_t want = tag | ((uint64_t)bi + 1);
+            SvcDesc *h = &host->desc[bi % kSvcRing];
+            t0 = memrealtime();
+            const uint64_t seq = __hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            timed_wait();
+            const uint64_t ready = __ballot(seq == want);
+            const uint32_t k = ~ready ? (uint32_t)__builtin_ctzll(~ready) : 64u;   // >= 1: lane 0 saw it
+            uint64_t recs = 0, bits = 0, n = 0, stride = 0;
+            if (lane < k) {   // fields only after their seq was seen (the wait above)
+                typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+                const u64x4 v = __builtin_nontemporal_load(reinterpret_cast<const u64x4 *>(&h->recs));
+                recs = v.x;
+                bits = v.y;
+                n = v.z;
+                stride = v.w;
+            }
+            timed_wait();
+            rt = memrealtime() - t0;
+            relay_spin(a.relay_delay_us);
+            reads += 2;
+            rticks += rt;
+            rmax = rt > rmax ? rt : rmax;
+            const uint64_t stops = __ballot(lane < k && n == kSvcStopN);
+            const uint32_t kk = stops ? (uint32_t)__builtin_ctzll(stops) + 1u : k;
+            SvcDesc *m = &dev->mir[bi % kSvcRing];
+            if (lane < kk) {   // write-through field stores, acknowledged before the seqs
+                __hip_atomic_store(&m->recs, recs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&m->bits, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&m->n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&m->stride, stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane < kk) {
+                __hip_atomic_store(&m->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dev->relay_clock[bi % kSvcRing] = memrealtime();
+            }
+            if (stops) {
+                stop = true;
+                stop_b = b + kk - 1;
+            }
+            b += kk;
+            descs += kk;
+            prog = true;
+            t_idle = memrealtime();
+        } else if (memrealtime() - t_idle > a.idle_ticks) {
+            if (lane == 0) {
+                SvcDesc *m = &dev->mir[b % kSvcRing];
+                __hip_atomic_store(&m->n, kSvcStopN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&m->seq, tag | ((uint64_t)b + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&host->status, kSvcIdleTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            stop = true;
+            stop_b = b++;
+            prog = true;
+        }
+        // forward the completions of batches every block has reported (none after the stop:
+        // the grid's exit tells the host)
+        while (!stop && f < b && f < stop_b) {
+            const uint64_t want = tag | ((uint64_t)f + 1);
+            bool ok = true;
+            for (uint32_t k = lane; k < G; k += 64)
+                ok = ok && __hip_atomic_load(&dev->done[f % kSvcRing][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+            if (__ballot(!ok)) break;
+            if (lane == 0) __hip_atomic_store(&host->done[f % kSvcRing], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ++f;
+            ++fwd;
+            prog = true;
+        }
+        if (!prog) __builtin_amdgcn_s_sleep(8);
+    }
+    if (lane == 0) {   // read by the host after the grid
+        dev->relay[kRelayProbeTicks] = probe;
+        dev->relay[kRelayReads] = reads;
+        dev->relay[kRelayReadTicks] = rticks;
+        dev->relay[kRelayReadMax] = rmax;
+        dev->relay[kRelayDescs] = descs;
+        dev->relay[kRelayForwarded] = fwd;
+        dev->relay[kRelayInline] = n_in;
     }
 }
 
@@ -843,18 +934,20 @@ __device__ void svc_relay(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks, ui
 // device mirror.  blocking: poll until the relay publishes it (bounded by a watchdog: the
 // relay itself publishes a stop descriptor after idle_ticks); otherwise one look.  Returns
 // false if the descriptor is not there yet.
-__device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blocking, uint64_t idle_ticks)
+__device__ bool svc_load(const SvcArgs &a, uint32_t b, bool blocking)
 {
     const uint32_t slot = b % kSvcRing;
-    SvcDesc *d = &mir[slot];
+    SvcDev *dev = a.dev;
+    SvcDesc *d = &dev->mir[slot];
     bool stop = false;
     const uint64_t want = s_svc_tag | ((uint64_t)b + 1);
     if (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
         if (!blocking) return false;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        __hip_atomic_fetch_add(&dev->relay[kRelayBlockWaits], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = memrealtime();
         while (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000000ull) {
-                __hip_atomic_store(&host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (memrealtime() - t0 > 2 * a.idle_ticks + 100000000ull) {
+                __hip_atomic_store(&a.host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 stop = true;
                 break;
             }
@@ -869,9 +962,7 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
 #elif HFV_SVC_ACQ == 3
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope (buffer_inv sc0 sc1: L1 and L2)
 #endif
-    if (blockIdx.x == 0)
-        __hip_atomic_store(&host->load_clock[slot], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x == 0) dev->load_clock[slot] = memrealtime();
     SvcSlot &s = s_svc[slot];
     const SvcSlot &p = s_svc[(b + kSvcRing - 1) % kSvcRing];
     s.base = b ? p.base + p.count : 0u;
@@ -894,49 +985,67 @@ __device__ bool svc_load(SvcShared *host, SvcDesc *mir, uint32_t b, bool blockin
         s.n = n;
         s.tile0 = t0;
         s.count = cnt;
-        if (s.count == 0) svc_complete(host, b);
+        if (s.count == 0) svc_complete(dev, a.tag, b);
     }
     __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return true;
 }
 
-// Batch 0 from the kernel arguments (SvcFirst): the slot svc_load would fill from the mirror,
-// filled before the prologue barrier by one thread of every block.
-__device__ void svc_load_first(SvcShared *host, const SvcFirst &f)
+// The batches in the kernel arguments (batches 0 .. n_inline - 1, posted before the launch):
+// wave 0 of every block fills their LDS slots before the prologue barrier, lane i batch i,
+// the slots' base tile numbers by a prefix sum over the lanes.  Their records were written
+// before the grid was launched, so no acquire fence is needed for them.
+__device__ void svc_load_inline(const SvcArgs &a, uint32_t lane)
 {
-    SvcSlot &s = s_svc[0];
-    s.base = 0;
-    s.done = 0;
-    s.recs = f.recs;
-    s.bits = f.bits;
-    s.stride = f.stride;
-    s.stop = f.n == kSvcStopN;
-    if (s.stop) {
-        s.count = 0;
-    } else {
-        uint64_t t0;
-        uint32_t cnt;
-        svc_share((f.n + 63) / 64, t0, cnt);
-        s.n = f.n;
-        s.tile0 = t0;
-        s.count = cnt;
-        if (s.count == 0) svc_complete(host, 0);
+    const uint32_t n_in = a.n_inline;
+    const uint64_t c0 = svc_cum(a.weights, blockIdx.x), c1 = svc_cum(a.weights, blockIdx.x + 1);
+    const uint64_t w = svc_cum(a.weights, gridDim.x);
+    uint32_t cnt = 0;
+    uint64_t t0 = 0;
+    SvcDescLite d = {0, 0, 0, 0};
+    bool stop = false;
+    if (lane < n_in) {
+        d = a.inl[lane];
+        stop = d.n == kSvcStopN;
+        if (!stop) {
+            const uint64_t nt = (d.n + 63) / 64;
+            t0 = nt * c0 / w;
+            cnt = (uint32_t)(nt * c1 / w - t0);
+        }
     }
-    s_svc_loaded = 1;
+    uint32_t incl = cnt;   // inclusive prefix sum of the counts over the lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane < n_in) {
+        SvcSlot &s = s_svc[lane];
+        s.base = incl - cnt;
+        s.count = cnt;
+        s.done = 0;
+        s.stop = stop;
+        s.recs = d.recs;
+        s.bits = d.bits;
+        s.n = d.n;
+        s.stride = d.stride;
+        s.tile0 = t0;
+        if (!stop && cnt == 0) svc_complete(a.dev, a.tag, lane);
+    }
+    if (lane == 0) s_svc_loaded = n_in;
 }
 
 // The wave has just entered batch b: if batch b + 1 is not loaded yet and nobody is loading,
 // take one look for its descriptor now, so the block's waves find it loaded when they reach
-// the end of batch b instead of waiting a PCIe round trip there.
-__device__ __forceinline__ void svc_prefetch(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks, uint32_t lane,
-                                             uint32_t b)
+// the end of batch b instead of waiting there.
+__device__ __forceinline__ void svc_prefetch(const SvcArgs &a, uint32_t lane, uint32_t b)
 {
     if (lane == 0 && __hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1) {
         uint32_t expect = 0;
         if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
             if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1)
-                (void)svc_load(host, mir, b + 1, false, idle_ticks);
+                (void)svc_load(a, b + 1, false);
             __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
@@ -944,8 +1053,8 @@ __device__ __forceinline__ void svc_prefetch(SvcShared *host, SvcDesc *mir, uint
 
 // Map block tile number g to its batch (mb: batch of the wave's previous claim, g only
 // grows).  Not blocking: kSvcPending if g lies in a batch the host has not posted yet.
-__device__ __forceinline__ SvcClaim svc_map(SvcShared *host, SvcDesc *mir, uint64_t idle_ticks, uint32_t lane,
-                                            uint32_t g, bool blocking, uint32_t &mb, const SvcTile &hint, SvcTile &t)
+__device__ __forceinline__ SvcClaim svc_map(const SvcArgs &a, uint32_t lane, uint32_t g, bool blocking, uint32_t &mb,
+                                            const SvcTile &hint, SvcTile &t)
 {
     if (g - hint.base < hint.count) {   // same batch as the wave's current tile: no LDS reads
         t = hint;
@@ -986,7 +1095,7 @@ __device__ __forceinline__ SvcClaim svc_map(SvcShared *host, SvcDesc *mir, uint6
                                                      __HIP_MEMORY_SCOPE_WORKGROUP)) {
                 r = 1;
                 if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == L &&
-                    !svc_load(host, mir, L, blocking, idle_ticks))
+                    !svc_load(a, L, blocking))
                     r = 2;
                 __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -995,11 +1104,11 @@ __device__ __forceinline__ SvcClaim svc_map(SvcShared *host, SvcDesc *mir, uint6
         if (r == 2 || (r == 0 && !blocking)) return kSvcPending;
         if (r == 0) {
             // watchdog: the loader is bounded by idle_ticks; never wait much longer here
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            const uint64_t now = memrealtime();
             if (!t_wait) t_wait = now;
-            if (now - t_wait > 2 * idle_ticks + 100000000ull) {
+            if (now - t_wait > 2 * a.idle_ticks + 100000000ull) {
                 if (lane == 0)
-                    __hip_atomic_store(&host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&a.host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return kSvcStop;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1007,67 +1116,43 @@ __device__ __forceinline__ SvcClaim svc_map(SvcShared *host, SvcDesc *mir, uint6
     }
 }
 
-// Count k verified tiles of batch b (count: the block's tiles in it) once their verdict
-// stores are acknowledged.  A wave defers this until its next claim leaves the batch (or
-// must wait for a descriptor), so the store-acknowledge wait is paid once per batch per
-// wave instead of once per tile.
-__device__ __forceinline__ void svc_count(SvcShared *host, uint32_t lane, uint32_t b, uint32_t count,
-                                          uint32_t k)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the verdict words are acknowledged
-    if (lane == 0) {
-        const uint32_t old =
-            __hip_atomic_fetch_add(&s_svc[b % kSvcRing].done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old + k == count) svc_complete(host, b);
-    }
-}
-
 template <int KEYSEL, int TAB>
-__global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__restrict__ tab,
-                                                         const uint32_t *__restrict__ ttab_img, SvcShared *host,
-                                                         SvcDesc *mir, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t idle_ticks, uint64_t tag, SvcFirst first,
-                                                         SvcWeights weights)
+__global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
-    if (HFV_SVC_SPAN && threadIdx.x == 0)
-        __hip_atomic_store(&host->span_entry[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    UniformKey ukey(tab);
+    SvcDev *dev = a.dev;
+    if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_entry[blockIdx.x] = memrealtime();
+    UniformKey ukey(a.tab);
+    const uint32_t inf_off = a.inf_off, hf_off = a.hf_off;
     if (threadIdx.x == 0) {
         s_svc_next = 0;
-        s_svc_loaded = 0;
         s_svc_lock = 0;
-        s_svc_tag = tag;
-        s_svc_c0 = svc_cum(weights, blockIdx.x);
-        s_svc_c1 = svc_cum(weights, blockIdx.x + 1);
-        s_svc_w = svc_cum(weights, gridDim.x);
-        if (first.stride) svc_load_first(host, first);   // batch 0 without waiting for the relay
+        s_svc_tag = a.tag;
+        s_svc_c0 = svc_cum(a.weights, blockIdx.x);
+        s_svc_c1 = svc_cum(a.weights, blockIdx.x + 1);
+        s_svc_w = svc_cum(a.weights, gridDim.x);
     }
-    // Block 0's last wave relays the host's descriptors into device memory for the grid's
-    // whole life.  It must not be alive at a barrier the other waves wait at (a wave still
+    if (threadIdx.x < 64) svc_load_inline(a, lane);   // the batches posted before the launch
+    // Block 0's last wave relays later-posted descriptors and forwards completions for the
+    // grid's life.  It must not be alive at a barrier the other waves wait at (a wave still
     // running holds the barrier), so it passes the table-fill barrier without filling and
     // starts relaying right after it.
     const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
     const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
-    if (!relay) fill_ttab_dma_issue_n<TAB>(ttab_img, threadIdx.x >> 6, nthr >> 6);
+    if (!relay) fill_ttab_dma_issue_n<TAB>(a.ttab_img, threadIdx.x >> 6, nthr >> 6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
-        if (!relay) fill_keys(tab, nthr);
+        if (!relay) fill_keys(a.tab, nthr);
     } else if constexpr (KEYSEL == kKeyselGather) {
-        fill_valid(tab);
+        fill_valid(a.tab);
     } else if constexpr (KEYSEL == kKeyselSched) {
-        if (!relay) fill_keys3(tab, nthr);
+        if (!relay) fill_keys3(a.tab, nthr);
     }
     __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(&host->blk_start[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    if (HFV_SVC_SPAN && threadIdx.x == 0)
-        __hip_atomic_store(&host->span_fill[blockIdx.x], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) dev->blk_start[blockIdx.x] = memrealtime();
+    if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_fill[blockIdx.x] = memrealtime();
     if (relay) {   // no barrier follows: the block's other waves go on without it
-        if (lane == 0) svc_relay(host, mir, idle_ticks, tag);
+        svc_relay(a, lane, gridDim.x);
         return;
     }
     const Lane l = lane_bases();
@@ -1076,9 +1161,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
     const UniformKey *ukp = KEYSEL == HFV_KEYSEL_ZERO ? &ukey : nullptr;
 
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // diagnostics: shader clock over the grid's life
-        __hip_atomic_store(&host->run_clock[0], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host->run_clock[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        dev->run_clock[0] = __builtin_amdgcn_s_memtime();
+        dev->run_clock[1] = memrealtime();
     }
     uint32_t mb = 0;
     SvcTile none;
@@ -1098,7 +1182,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         return g;
     };
     SvcTile cur;
-    if (svc_map(host, mir, idle_ticks, lane, wave_uniform(claim()), true, mb, none, cur) != kSvcFound) return;
+    if (svc_map(a, lane, wave_uniform(claim()), true, mb, none, cur) != kSvcFound) return;
     uint32_t gq = HFV_SVC_AHEAD ? claim() : 0u;   // the next tile's number (lane 0), read one iteration later
     // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
     // out as ONE scattered write-through store, issued at the top of the iteration after the
@@ -1115,7 +1199,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         if (k && lane == 0) {
             const uint32_t old =
                 __hip_atomic_fetch_add(&s_svc[b % kSvcRing].done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old + k == cnt) svc_complete(host, b);
+            if (old + k == cnt) svc_complete(dev, a.tag, b);
         }
     };
     auto store_stash = [&]() {
@@ -1125,7 +1209,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         stashed = 0;
     };
     RecWords rc = load_tile(cur, lane, inf_off, hf_off);
-    svc_prefetch(host, mir, idle_ticks, lane, cur.b);
+    svc_prefetch(a, lane, cur.b);
     SvcProf prof;
     const uint64_t prof_t0 = HFV_SVC_PROF ? __builtin_amdgcn_s_memtime() : 0;
     prof.start();
@@ -1147,7 +1231,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
         // per-interface keys: this tile's key rows, issued BEFORE the next tile's record loads
         // (vmcnt retires in order: a row wait must not also wait for those HBM loads)
         GatherKey gk;
-        if constexpr (KEYSEL == kKeyselGather) gk.issue(tab, rec_key_slot(rc));
+        if constexpr (KEYSEL == kKeyselGather) gk.issue(a.tab, rec_key_slot(rc));
         uint32_t g;
         if constexpr (HFV_SVC_AHEAD) {
             g = wave_uniform(gq);
@@ -1156,7 +1240,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
             g = wave_uniform(claim());
         }
         SvcTile nx;
-        SvcClaim c = svc_map(host, mir, idle_ticks, lane, g, false, mb, cur, nx);
+        SvcClaim c = svc_map(a, lane, g, false, mb, cur, nx);
         if (c != kSvcFound) nx = cur;
         RecWords rn = load_tile(nx, lane, inf_off, hf_off);
         prof.mark(1);
@@ -1200,24 +1284,21 @@ __global__ __launch_bounds__(1024) void k_verify_service(const DevKeyTable *__re
                 flush = false;
             }
             if (c == kSvcPending) {
-                c = svc_map(host, mir, idle_ticks, lane, g, true, mb, none, nx);
+                c = svc_map(a, lane, g, true, mb, none, nx);
                 if (c == kSvcFound) rn = load_tile(nx, lane, inf_off, hf_off);
             }
         }
         prof.mark(4);
         if (c == kSvcStop) break;
-        if (nx.b != cur.b) svc_prefetch(host, mir, idle_ticks, lane, nx.b);
+        if (nx.b != cur.b) svc_prefetch(a, lane, nx.b);
         cur = nx;
         rc = rn;
     }
-    prof.flush(host, lane, prof_t0);
-    if (HFV_SVC_SPAN && lane == 0)
-        __hip_atomic_store(&host->span_exit[blockIdx.x * 16 + (threadIdx.x >> 6)], __builtin_amdgcn_s_memrealtime(),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    prof.flush(a.host, lane, prof_t0);
+    if (HFV_SVC_SPAN && lane == 0) dev->span_exit[blockIdx.x * 16 + (threadIdx.x >> 6)] = memrealtime();
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        __hip_atomic_store(&host->run_clock[2], __builtin_amdgcn_s_memtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host->run_clock[3], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        dev->run_clock[2] = __builtin_amdgcn_s_memtime();
+        dev->run_clock[3] = memrealtime();
     }
 }
 
@@ -1236,10 +1317,8 @@ int launch_debug_spin(void *stream, uint32_t us)
     return (int)hipGetLastError();
 }
 
-int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keysel, SvcShared *host, SvcDesc *mir,
-                          uint32_t inf_off,
-                          uint32_t hf_off, uint64_t idle_ticks, uint64_t tag, SvcFirst first, SvcWeights weights,
-                          void *stream, void *ev_start, void *ev_stop, unsigned *grid_out)
+int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
+                          void *ev_stop, unsigned *grid_out)
 {
     // Per-interface keys (config 3).  Default: three LDS rows per slot beside all four round
     // tables, rounds 3..10's keys expanded per packet (SchedKey): bank-conflict cycles 1.37 M ->
@@ -1259,8 +1338,7 @@ int launch_verify_service(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     if (grid > kSvcMaxBlocks) grid = kSvcMaxBlocks;
     *grid_out = grid;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, host, mir, inf_off, hf_off,
-                          idle_ticks, tag, first, weights);
+                          (hipEvent_t)ev_stop, 0u, args);
     return (int)hipGetLastError();
 }
 

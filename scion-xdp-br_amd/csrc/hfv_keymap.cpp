@@ -77,8 +77,13 @@ static int mkdir_p(const char *path)
     return 0;
 }
 
-// Open (creating if asked) and map the file; returns the fd, the mapping in *out.
-static int map_file(const char *path, bool create, bool writable, KeymapFile **out)
+// Size of a map pinned by the round-2 build, before the far[] entries of HASH8 mode: refused
+// with its own error (-EPROTO, "old key map layout") instead of a bare -EINVAL.
+constexpr size_t kOldKeymapSize = 64 + HFV_MAX_KEYS * 192;
+
+// Open (creating if asked) and map the file; returns the fd, the mapping in *out; *fresh (if
+// given): the file had no map in it yet (created now, or still all zero).
+static int map_file(const char *path, bool create, bool writable, KeymapFile **out, bool *fresh = nullptr)
 {
     if (create) {
         int rc = mkdir_p(path);
@@ -93,15 +98,17 @@ static int map_file(const char *path, bool create, bool writable, KeymapFile **o
         if (ftruncate(fd, sizeof(KeymapFile)) != 0) { int e = -errno; close(fd); return e; }
     } else if ((size_t)st.st_size != sizeof(KeymapFile)) {
         close(fd);
-        return -EINVAL;
+        return (size_t)st.st_size == kOldKeymapSize ? -EPROTO : -EINVAL;
     }
     void *m = mmap(nullptr, sizeof(KeymapFile), writable ? PROT_READ | PROT_WRITE : PROT_READ, MAP_SHARED, fd, 0);
     if (m == MAP_FAILED) { int e = -errno; close(fd); return e; }
     KeymapFile *km = (KeymapFile *)m;
+    if (fresh) *fresh = false;
     if (writable && memcmp(km->magic, kMagic, 8) != 0) {
         if (st.st_size != 0 && km->magic[0] != 0) { munmap(m, sizeof(KeymapFile)); close(fd); return -EINVAL; }
         memcpy(km->magic, kMagic, 8);
         km->version = 1;
+        if (fresh) *fresh = true;
     } else if (!writable && memcmp(km->magic, kMagic, 8) != 0) {
         munmap(m, sizeof(KeymapFile));
         close(fd);
@@ -168,11 +175,23 @@ void keymap_close(const void *mapping)
 int keymap_create(const char *path, uint32_t mode)
 {
     KeymapFile *km;
-    int fd = map_file(path, true, true, &km);   // header written under the flock, slots untouched
+    bool fresh = false;
+    int fd = map_file(path, true, true, &km, &fresh);   // header written under the flock, slots untouched
     if (fd < 0) return fd;
-    if (entries(km) == 0) km->mode = mode;       // an existing map with keys keeps its mode
+    // only a map created now takes the mode: an existing one keeps its own, keys or not (an
+    // `attach --key-slots` map stays a 256-slot map when `key add` opens it)
+    if (fresh) km->mode = mode;
     unmap_file(fd, km);
     return 0;
+}
+
+// fail() for a map that could not be opened: an old layout gets its own message.
+static int open_fail(int rc, const char *path)
+{
+    if (rc == -EPROTO)
+        return fail(rc, "key map %s has an old layout (%zu bytes, before the HASH8 entries); remove it and add the "
+                        "keys again", path, kOldKeymapSize);
+    return fail(rc, "cannot open key map %s", path);
 }
 
 }  // namespace hfv
@@ -196,7 +215,7 @@ int hfv_keymap_update(const char *path, uint32_t index, const struct hop_key *hk
     if (!path || !hk) return fail(-EINVAL, "null argument");
     KeymapFile *km;
     int fd = map_file(path, true, true, &km);   // a map created here is a slots map
-    if (fd < 0) return fail(fd, "cannot open key map %s", path);
+    if (fd < 0) return open_fail(fd, path);
     const bool hash8 = km->mode == HFV_KEYMAP_HASH8;
     int far = -1, free_far = -1;
     for (int f = 0; f < kFar; ++f) {
@@ -231,7 +250,7 @@ int hfv_keymap_erase(const char *path, uint32_t index)
     if (!path) return fail(-EINVAL, "null argument");
     KeymapFile *km;
     int fd = map_file(path, false, true, &km);
-    if (fd < 0) return fail(fd, "cannot open key map %s", path);
+    if (fd < 0) return open_fail(fd, path);
     int rc = 0, far = -1;
     for (int f = 0; f < kFar; ++f)
         if (km->far[f].used && km->far[f].index == index) far = f;
@@ -257,14 +276,14 @@ int hfv_keymap_create(const char *path)
 {
     if (!path) return fail(-EINVAL, "null argument");
     int rc = keymap_create(path, HFV_KEYMAP_SLOTS);
-    return rc ? fail(rc, "cannot create key map %s", path) : 0;
+    return rc == -EPROTO ? open_fail(rc, path) : rc ? fail(rc, "cannot create key map %s", path) : 0;
 }
 
 int hfv_keymap_create_mode(const char *path, int mode)
 {
     if (!path || (mode != HFV_KEYMAP_SLOTS && mode != HFV_KEYMAP_HASH8)) return fail(-EINVAL, "bad argument");
     int rc = keymap_create(path, (uint32_t)mode);
-    return rc ? fail(rc, "cannot create key map %s", path) : 0;
+    return rc == -EPROTO ? open_fail(rc, path) : rc ? fail(rc, "cannot create key map %s", path) : 0;
 }
 
 int hfv_keymap_mode(const char *path)
@@ -272,7 +291,7 @@ int hfv_keymap_mode(const char *path)
     if (!path) return fail(-EINVAL, "null argument");
     const void *m;
     int rc = keymap_open_ro(path, &m);
-    if (rc) return fail(rc, "cannot open key map %s", path);
+    if (rc) return open_fail(rc, path);
     const int mode = (int)__atomic_load_n(&((const KeymapFile *)m)->mode, __ATOMIC_ACQUIRE);
     keymap_close(m);
     return mode;
@@ -283,7 +302,7 @@ int hfv_keymap_list(const char *path, uint32_t *indices, struct hop_key *keys, s
     if (!path || !count || (cap && (!indices || !keys))) return fail(-EINVAL, "null argument");
     const void *m;
     int rc = keymap_open_ro(path, &m);
-    if (rc) return fail(rc, "cannot open key map %s", path);
+    if (rc) return open_fail(rc, path);
     const KeymapFile *km = (const KeymapFile *)m;
     static thread_local KeymapFile snap;
     for (;;) {   // the seqlock reader over the whole file
@@ -319,7 +338,7 @@ int hfv_keymap_read(const char *path, struct hop_key *slots, uint32_t *valid)
     if (!path || !slots || !valid) return fail(-EINVAL, "null argument");
     const void *m;
     int rc = keymap_open_ro(path, &m);
-    if (rc) return fail(rc, "cannot open key map %s", path);
+    if (rc) return open_fail(rc, path);
     keymap_snapshot(m, slots, valid);
     keymap_close(m);
     return 0;

@@ -29,6 +29,7 @@ REC_INF_OFF = 40
 REC_HF_OFF = 48
 REC_SIZE = 64
 SVC_RING = 256   # resident-service descriptor ring (kSvcRing, csrc/hfv_internal.h)
+SVC_INLINE = 64  # descriptors a service grid gets in its kernel arguments (kSvcInline)
 BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic HBM bytes per verified record
 
 
@@ -589,6 +590,30 @@ class Ctx:
         us = lambda t: round((int(t) - r0) / 100.0, 2) if t else None   # noqa: E731
         return {"loop_us": us(r1), "relay_us": [us(clk[SVC_RING + 4 + i]) for i in range(nbatches + 1)],
                 "load_us": [us(clk[i]) for i in range(nbatches + 1)]}
+
+    def service_relay(self):
+        """Diagnostic: the last service grid's relay counters (hfv_debug_service_relay) -- how the
+        host link behaved for it: the PCIe round trip probed at grid start and the longest host
+        read (us), host reads, descriptors relayed beyond the inline ones, completions forwarded,
+        waits of a block for a descriptor, descriptors in the kernel arguments."""
+        v = (ctypes.c_uint64 * 8)()
+        L = lib()
+        L.hfv_debug_service_relay.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        if L.hfv_debug_service_relay(self._h, v) != 0:
+            return None
+        x = [int(t) for t in v]
+        return {"probe_rtt_us": round(x[0] / 100.0, 2), "host_reads": x[1],
+                "read_rtt_mean_us": round(x[2] / 100.0 / x[1], 2) if x[1] else None,
+                "read_rtt_max_us": round(x[3] / 100.0, 2), "relayed": x[4], "forwarded": x[5],
+                "block_waits": x[6], "inline": x[7]}
+
+    @staticmethod
+    def debug_relay_delay(us):
+        """Test-only: every host read of later service grids' relay wave takes `us` microseconds
+        longer (a slow PCIe link); 0 = off."""
+        L = lib()
+        L.hfv_debug_relay_delay.argtypes = [ctypes.c_uint32]
+        _check(L.hfv_debug_relay_delay(us))
 
     def service_set_timing(self, enable):
         """Launch later service grids with (True) or without the dispatch timing events."""

@@ -195,6 +195,43 @@ def test_cli_attach_detach(pin_dir, tmp_path):
     assert run("detach", "no-such-br", env=env).returncode != 0
 
 
+def test_cli_key_slots_map_keeps_its_mode(pin_dir, tmp_path):
+    """a map that `attach --key-slots` created stays a 256-slot map when
+    `key add` opens it (only a map created by `key add` itself takes the reference's HASH8
+    mode), so per-interface keys (config 3) can be installed through the CLI past 8 entries,
+    and an index the data plane never reads (>= 256) is refused."""
+    if not os.path.exists(LOADER):
+        pytest.skip("hfv-loader not built")
+    import json
+    topo = {"border_routers": {"br1-s": {"internal_addr": "10.2.0.1:31002", "interfaces": {
+        "1": {"underlay": {"public": "10.1.1.2:50000", "remote": "10.1.1.1:50000"}}}}}}
+    tp = tmp_path / "topology.json"
+    tp.write_text(json.dumps(topo))
+    conf = tmp_path / "br1.toml"
+    conf.write_text('self = "br1-s"\ntopology = "%s"\ninternal_interfaces = [\n    {ip = "10.2.0.1", port = 31002}\n]\n' % tp)
+    env = dict(os.environ)
+    r = run("attach", str(conf), "--key-slots", env=env)
+    assert r.returncode == 0, r.stderr
+    path = hfv.keymap_path("br1-s")
+    assert hfv.keymap_mode(path) == hfv.KEYMAP_SLOTS
+    for i in list(range(12)) + [255]:
+        r = run("key", "add", "br1-s", str(i), "MTExMTExMTExMTExMTExMQ==", env=env)
+        assert r.returncode == 0, r.stderr
+    assert hfv.keymap_mode(path) == hfv.KEYMAP_SLOTS
+    assert sorted(hfv.keymap_read(path)) == list(range(12)) + [255]
+    bad = run("key", "add", "br1-s", "256", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert bad.returncode != 0
+    # ADVICE r03 (low): a map pinned by the round-2 build (before the HASH8 entries) is refused
+    # with its own message instead of a bare EINVAL
+    old = pin_dir / "br-old" / "mac_key_map"
+    old.parent.mkdir()
+    old.write_bytes(b"HFVKMAP1" + bytes(64 + 256 * 192 - 8))
+    with pytest.raises(hfv.HfvError, match="old layout"):
+        hfv.keymap_read(str(old))
+    bad = run("key", "add", "br-old", "0", "MTExMTExMTExMTExMTExMQ==", env=env)
+    assert bad.returncode != 0
+
+
 def test_brconfig_rejects_tables_past_capacity(pin_dir):
     """publish and read check the table counts against the fixed capacity, so a
     corrupt or foreign pinned file cannot drive the compile loops past the arrays."""

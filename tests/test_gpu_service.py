@@ -364,3 +364,87 @@ def test_service_bad_arguments(ctx):
         ctx.service_submit(recs, 4, bits, stride=40)
     with pytest.raises(hfv.HfvError):
         ctx.service_wait(12345)
+
+
+def _grid_ms(ctx, posts):
+    """One hfv_service_run_async grid over the prepared batches; its event-timed lifetime."""
+    ctx.service_set_timing(True)
+    ctx.service_run_async(posts)
+    torch.cuda.synchronize()
+    return ctx.service_stop()
+
+
+@pytest.mark.parametrize("k,n", [(20, 1 << 20), (100, 1 << 18)], ids=["k20_2e20", "k100_2e18"])
+def test_service_grid_ignores_host_round_trips(ctx, k, n):
+    """the resident grid must not run at the pace of host-memory round trips.
+    A debug hook makes every host read of the relay wave take 30 us longer (a slow PCIe link,
+    as on the driver's round-3 box, whose service grids ran at ~42 us per 2^20 batch).  K = 20
+    batches all travel in the kernel arguments; K = 100 puts 36 behind the relay's read-ahead.
+    Either way the delayed grids stay within 10 % of the undelayed ones, no block ever waits for
+    a descriptor, and the verdicts equal the launch path's."""
+    ctx.key_add(0, orc.KEY_1111)
+    R = 4
+    recs = [torch.empty((n, 64), dtype=torch.uint8, device=DEV) for _ in range(R)]
+    want = []
+    for i, r in enumerate(recs):
+        ctx.gen_records(r, n, orc.SEED_RECORDS, first_index=i * n)
+        w = new_bits(n)
+        ctx.verify_records(r, n, w)
+        want.append(w)
+    outs = [new_bits(n, fill=-1) for _ in range(k)]
+    torch.cuda.synchronize()
+    posts = ctx.service_batches([(recs[i % R], n, outs[i]) for i in range(k)])
+    times = {0: [], 30: []}
+    try:
+        _grid_ms(ctx, posts)   # warm-up grid
+        for _ in range(3):
+            for us in (0, 30):
+                hfv.Ctx.debug_relay_delay(us)
+                for o in outs:
+                    o.fill_(-1)
+                torch.cuda.synchronize()
+                times[us].append(_grid_ms(ctx, posts))
+                rel = ctx.service_relay()
+                assert rel["block_waits"] == 0, rel
+                assert rel["inline"] == min(k + 1, hfv.SVC_INLINE), rel
+                assert rel["relayed"] == max(0, k + 1 - hfv.SVC_INLINE), rel
+                if us:
+                    assert rel["read_rtt_max_us"] >= us, rel   # the hook really delayed the reads
+                for i, o in enumerate(outs):
+                    assert torch.equal(o, want[i % R]), f"batch {i}"
+    finally:
+        hfv.Ctx.debug_relay_delay(0)
+    fast, slow = sorted(times[0])[1], sorted(times[30])[1]
+    print(f"K={k} n={n}: grids {times}, medians {fast:.4f} / {slow:.4f} ms")
+    assert slow <= 1.10 * fast, times
+
+
+def test_service_live_submits_with_slow_host_link(ctx):
+    """The relay's other duties under a slow host link (30 us extra per host read): descriptors
+    posted one at a time to a running grid, and completions forwarded to the host ring so that
+    hfv_service_wait and ring-slot reuse (more batches than ring slots) still work."""
+    g = orc.load_golden("hf_single.npz")
+    n = len(g["records"])
+    d = dev(g["records"])
+    ctx.key_add(0, orc.KEY_1111)
+    hk, valid = orc.key_table(orc.KEY_1111)
+    want = orc.verify_records(g["records"], hk, valid, 0)
+    try:
+        hfv.Ctx.debug_relay_delay(30)
+        outs = [new_bits(n, fill=-1) for _ in range(hfv.SVC_RING + 40)]
+        torch.cuda.synchronize()
+        ctx.service_start()
+        ts = []
+        for i, o in enumerate(outs):
+            ts.append(ctx.service_submit(d, n, o))
+            if i % 50 == 0:
+                ctx.service_wait(ts[-1], 20000)    # a forwarded completion while the grid runs
+                assert ctx.service_poll(ts[-1])
+        ctx.service_wait(ts[-1], 20000)
+        for o in outs:
+            assert np.array_equal(bits_np(o, n), want)
+        ctx.service_stop()
+        rel = ctx.service_relay()
+        assert rel["relayed"] >= len(outs) and rel["forwarded"] >= hfv.SVC_RING, rel
+    finally:
+        hfv.Ctx.debug_relay_delay(0)

@@ -448,3 +448,36 @@ def test_service_live_submits_with_slow_host_link(ctx):
         assert rel["relayed"] >= len(outs) and rel["forwarded"] >= hfv.SVC_RING, rel
     finally:
         hfv.Ctx.debug_relay_delay(0)
+
+
+@pytest.mark.parametrize("k", [3, 6, 9])
+def test_service_dynamic_tail_ragged(ctx, k):
+    """The dynamic tail of a run grid (the last 1-2 batches claimed in chunks from device-scope
+    counters, SvcArgs::dyn_from): ragged batch sizes (a partial last tile, chunks that end at a
+    batch's end), back-to-back grids (the per-grid scratch alternates), verdicts equal to the
+    launch path's for every batch; with HFV_SVC_DYN unset the tail is on at these sizes."""
+    ctx.key_add(0, orc.KEY_1111)
+    base = 1 << 19
+    sizes = [base + 37 * i + (i % 3) for i in range(k)]
+    recs = torch.empty((max(sizes), 64), dtype=torch.uint8, device=DEV)
+    ctx.gen_records(recs, max(sizes), orc.SEED_RECORDS)
+    want = []
+    for n in sizes:
+        w = new_bits(n)
+        ctx.verify_records(recs, n, w)
+        want.append(w)
+    outs = [new_bits(n, fill=-1) for n in sizes]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for o in outs:
+            o.fill_(-1)
+        torch.cuda.synchronize()
+        ts = ctx.service_run_async([(recs, n, o) for n, o in zip(sizes, outs)])
+        torch.cuda.synchronize()
+        for t in ts:
+            assert ctx.service_poll(t)
+        assert ctx.service_stop() > 0
+        for i, (o, w) in enumerate(zip(outs, want)):
+            assert torch.equal(o, w), f"batch {i}"
+    rel = ctx.service_relay()
+    assert rel["block_waits"] == 0 and rel["relayed"] == 0, rel

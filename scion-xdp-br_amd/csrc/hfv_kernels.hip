@@ -846,8 +846,8 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
     uint64_t t0 = memrealtime();
     uint64_t probe_v = __hip_atomic_load(&host->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     timed_wait();
+    relay_spin(a.relay_delay_us);   // (the test hook's delay counts as part of the round trip)
     const uint64_t probe = memrealtime() - t0 + (probe_v == 0x5eedull ? 1 : 0);
-    relay_spin(a.relay_delay_us);
     uint64_t t_idle = memrealtime();
     while (!stop) {
         bool prog = false;
@@ -856,8 +856,8 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
         t0 = memrealtime();
         if (lane == 0) s0 = __hip_atomic_load(&host->desc[b % kSvcRing].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         timed_wait();
-        uint64_t rt = memrealtime() - t0;
         relay_spin(a.relay_delay_us);
+        uint64_t rt = memrealtime() - t0;
         ++reads;
         rticks += rt;
         rmax = rt > rmax ? rt : rmax;
@@ -881,8 +881,8 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
                 stride = v.w;
             }
             timed_wait();
-            rt = memrealtime() - t0;
             relay_spin(a.relay_delay_us);
+            rt = memrealtime() - t0;
             reads += 2;
             rticks += rt;
             rmax = rt > rmax ? rt : rmax;

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of library builds on the bench headline (one bench.py process per run,
-HFV_LIB selecting the build):  python scripts/ab_libs.py ROUNDS lib1.so lib2.so ... [-- bench args]
+HFV_LIB selecting the build):  python scripts/ab_libs.py ROUNDS lib1.so lib2.so[@VAR=VAL,...] ... [-- bench args]
+(a spec's @VAR=VAL,... sets environment variables for that run: the same build with a switch)
 Prints one line per run: build, value (Mpkt/s), grid ms, shader MHz, launch-path Mpkt/s."""
 import json
 import os
@@ -20,16 +21,18 @@ def main():
     bench = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-extras", "--cpu-budget", "0", "--no-host-e2e"] + \
         (extra or ["--steps", "20", "--warmup", "5"])
     for r in range(rounds):
-        for lib in libs:
+        for spec in libs:
+            lib, _, envs = spec.partition("@")
             env = dict(os.environ, HFV_LIB=os.path.abspath(lib))
+            env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
             p = subprocess.run(bench, capture_output=True, text=True, env=env, timeout=240)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
             if p.returncode != 0 or not line:
-                print(f"{r} {os.path.basename(lib)} FAILED rc={p.returncode} {p.stderr[-400:]}", flush=True)
+                print(f"{r} {spec} FAILED rc={p.returncode} {p.stderr[-400:]}", flush=True)
                 sys.exit(1)
             d = json.loads(line[0])
             s = d["service"] or {}
-            print(f"{r} {os.path.basename(lib):24s} value {d['value']:9.1f} grid_ms {s.get('grid_ms')} "
+            print(f"{r} {os.path.basename(lib) + ('@' + envs if envs else ''):32s} value {d['value']:9.1f} grid_ms {s.get('grid_ms')} "
                   f"mhz {s.get('shader_mhz')} launch {d['per_launch']['mpkts']:9.1f}", flush=True)
 
 

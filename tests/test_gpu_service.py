@@ -408,8 +408,12 @@ def test_service_grid_ignores_host_round_trips(ctx, k, n):
                 assert rel["block_waits"] == 0, rel
                 assert rel["inline"] == min(k + 1, hfv.SVC_INLINE), rel
                 assert rel["relayed"] == max(0, k + 1 - hfv.SVC_INLINE), rel
-                if us:
-                    assert rel["read_rtt_max_us"] >= us, rel   # the hook really delayed the reads
+                if us:   # the hook really delayed the host reads (the probe at grid start, and the relay's)
+                    assert rel["probe_rtt_us"] >= us, rel
+                    if k + 1 > hfv.SVC_INLINE:
+                        assert rel["host_reads"] > 0 and rel["read_rtt_max_us"] >= us, rel
+                if k + 1 <= hfv.SVC_INLINE:
+                    assert rel["host_reads"] == 0, rel   # every batch and the stop were inline
                 for i, o in enumerate(outs):
                     assert torch.equal(o, want[i % R]), f"batch {i}"
     finally:

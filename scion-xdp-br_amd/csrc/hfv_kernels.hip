@@ -668,6 +668,27 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
 // and the wave that completes the block's share stores the ticket into dev->done[slot][k]
 // (svc_complete, device memory); the relay wave forwards a batch's completion to the host
 // once every block has reported it.
+// The service kernel's argument struct, read in place in the kernarg segment.
+typedef const __attribute__((address_space(4))) SvcArgs *KArgs;
+
+__device__ __forceinline__ SvcDescLite karg_desc(KArgs a, uint32_t i)
+{
+    SvcDescLite d;
+    d.recs = a->inl[i].recs;
+    d.bits = a->inl[i].bits;
+    d.n = a->inl[i].n;
+    d.stride = a->inl[i].stride;
+    return d;
+}
+// svc_cum over the kernel argument's weights
+__device__ __forceinline__ uint64_t karg_cum(KArgs a, uint64_t k)
+{
+    SvcWeights w;
+    for (int x = 0; x < 8; ++x) w.w[x] = a->weights.w[x];
+    w.w0 = a->weights.w0;
+    return svc_cum(w, k);
+}
+
 struct SvcSlot {
     uint32_t base, count;   // block tile numbers [base, base + count)
     uint32_t done, stop;    // tiles of the piece this block has verified; 1: exit descriptor
@@ -786,7 +807,7 @@ struct SvcProf {
 // block 0 reads it); no grid-wide atomic (256 blocks on one counter serialise at the
 // memory-side atomic unit: ~40 us per batch at 256 blocks, profiles/r01/service/) and no
 // host-memory store whose acknowledgement a compute wave would wait for.
-__device__ void svc_complete(SvcDev *dev, uint64_t tag, uint32_t b)
+__device__ __attribute__((noinline)) void svc_complete(SvcDev *dev, uint64_t tag, uint32_t b)
 {
     dev->blk_fin[blockIdx.x] = __builtin_amdgcn_s_memrealtime();   // read by the host after the grid
     __hip_atomic_store(&dev->done[b % kSvcRing][blockIdx.x], tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
@@ -795,13 +816,13 @@ __device__ void svc_complete(SvcDev *dev, uint64_t tag, uint32_t b)
 
 // A piece of dynamic batch b is verified (one lane): the batch's verified-tile count; the
 // block whose piece completes it publishes the batch (dev->bfin).
-__device__ void dyn_done(const SvcArgs &a, uint32_t b, uint32_t k)
+__device__ __attribute__((noinline)) void dyn_done(KArgs a, uint32_t b, uint32_t k)
 {
-    SvcArea *area = &a.dev->area[a.launch & 1];
-    const uint32_t T = (uint32_t)((a.inl[b].n + 63) / 64);
+    SvcArea *area = &a->dev->area[a->launch & 1];
+    const uint32_t T = (uint32_t)((a->inl[b].n + 63) / 64);
     const uint32_t old = __hip_atomic_fetch_add(&area->bdone[b], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old + k == T)
-        __hip_atomic_store(&a.dev->bfin[b % kSvcRing], a.tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
+        __hip_atomic_store(&a->dev->bfin[b % kSvcRing], a->tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -828,13 +849,13 @@ __device__ __forceinline__ void relay_spin(uint32_t us)
 // idle_ticks without a new post it publishes a stop descriptor.  It leaves as soon as it has
 // published a stop: a grid that exits on its stop has verified everything before it, and the
 // host infers those completions from the grid's exit, so the relay never holds the grid open.
-__device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
+__device__ __attribute__((noinline)) void svc_relay(KArgs a, uint32_t lane, uint32_t G)
 {
-    SvcShared *host = a.host;
-    SvcDev *dev = a.dev;
-    const uint64_t tag = a.tag;
-    const uint32_t n_in = a.n_inline;
-    bool stop = n_in && a.inl[n_in - 1].n == kSvcStopN;
+    SvcShared *host = a->host;
+    SvcDev *dev = a->dev;
+    const uint64_t tag = a->tag;
+    const uint32_t n_in = a->n_inline;
+    bool stop = n_in && a->inl[n_in - 1].n == kSvcStopN;
     uint32_t b = n_in;                       // next batch to relay
     uint32_t stop_b = stop ? n_in - 1 : ~0u;
     uint32_t f = 0;                          // next batch whose completion is forwarded
@@ -846,7 +867,7 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
     uint64_t t0 = memrealtime();
     uint64_t probe_v = __hip_atomic_load(&host->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     timed_wait();
-    relay_spin(a.relay_delay_us);   // (the test hook's delay counts as part of the round trip)
+    relay_spin(a->relay_delay_us);   // (the test hook's delay counts as part of the round trip)
     const uint64_t probe = memrealtime() - t0 + (probe_v == 0x5eedull ? 1 : 0);
     uint64_t t_idle = memrealtime();
     while (!stop) {
@@ -856,7 +877,7 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
         t0 = memrealtime();
         if (lane == 0) s0 = __hip_atomic_load(&host->desc[b % kSvcRing].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         timed_wait();
-        relay_spin(a.relay_delay_us);
+        relay_spin(a->relay_delay_us);
         uint64_t rt = memrealtime() - t0;
         ++reads;
         rticks += rt;
@@ -881,7 +902,7 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
                 stride = v.w;
             }
             timed_wait();
-            relay_spin(a.relay_delay_us);
+            relay_spin(a->relay_delay_us);
             rt = memrealtime() - t0;
             reads += 2;
             rticks += rt;
@@ -908,7 +929,7 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
             descs += kk;
             prog = true;
             t_idle = memrealtime();
-        } else if (memrealtime() - t_idle > a.idle_ticks) {
+        } else if (memrealtime() - t_idle > a->idle_ticks) {
             if (lane == 0) {
                 SvcDesc *m = &dev->mir[b % kSvcRing];
                 __hip_atomic_store(&m->n, kSvcStopN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -952,20 +973,20 @@ __device__ void svc_relay(const SvcArgs &a, uint32_t lane, uint32_t G)
 // device mirror.  blocking: poll until the relay publishes it (bounded by a watchdog: the
 // relay itself publishes a stop descriptor after idle_ticks); otherwise one look.  Returns
 // false if the descriptor is not there yet.
-__device__ bool svc_load(const SvcArgs &a, uint32_t b, bool blocking)
+__device__ __attribute__((noinline)) bool svc_load(KArgs a, uint32_t b, bool blocking)
 {
     const uint32_t slot = b % kSvcRing;
-    SvcDev *dev = a.dev;
+    SvcDev *dev = a->dev;
     SvcDesc *d = &dev->mir[slot];
     bool stop = false;
     const uint64_t want = s_svc_tag | ((uint64_t)b + 1);
     if (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
         if (!blocking) return false;
-        __hip_atomic_fetch_add(&dev->area[a.launch & 1].block_waits, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&dev->area[a->launch & 1].block_waits, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = memrealtime();
         while (__hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-            if (memrealtime() - t0 > 2 * a.idle_ticks + 100000000ull) {
-                __hip_atomic_store(&a.host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (memrealtime() - t0 > 2 * a->idle_ticks + 100000000ull) {
+                __hip_atomic_store(&a->host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 stop = true;
                 break;
             }
@@ -1005,7 +1026,7 @@ __device__ bool svc_load(const SvcArgs &a, uint32_t b, bool blocking)
         s.n = n;
         s.tile0 = t0;
         s.count = cnt;
-        if (s.count == 0) svc_complete(dev, a.tag, b);
+        if (s.count == 0) svc_complete(dev, a->tag, b);
     }
     __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return true;
@@ -1015,17 +1036,17 @@ __device__ bool svc_load(const SvcArgs &a, uint32_t b, bool blocking)
 // wave 0 of every block fills their LDS slots before the prologue barrier, lane i batch i,
 // the slots' base tile numbers by a prefix sum over the lanes.  Their records were written
 // before the grid was launched, so no acquire fence is needed for them.
-__device__ void svc_load_inline(const SvcArgs &a, uint32_t lane)
+__device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane)
 {
-    const uint32_t n_in = a.n_inline;
-    const uint64_t c0 = svc_cum(a.weights, blockIdx.x), c1 = svc_cum(a.weights, blockIdx.x + 1);
-    const uint64_t w = svc_cum(a.weights, gridDim.x);
+    const uint32_t n_in = a->n_inline;
+    const uint64_t c0 = karg_cum(a, blockIdx.x), c1 = karg_cum(a, blockIdx.x + 1);
+    const uint64_t w = karg_cum(a, gridDim.x);
     uint32_t cnt = 0;
     uint64_t t0 = 0;
     SvcDescLite d = {0, 0, 0, 0};
     bool stop = false;
     if (lane < n_in) {
-        d = a.inl[lane];
+        d = karg_desc(a, lane);
         stop = d.n == kSvcStopN;
         if (!stop) {
             const uint64_t nt = (d.n + 63) / 64;
@@ -1039,7 +1060,7 @@ __device__ void svc_load_inline(const SvcArgs &a, uint32_t lane)
         const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
         if ((int)lane >= o) incl += y;
     }
-    const uint32_t n_st = n_in < a.dyn_from ? n_in : a.dyn_from;   // static pieces (batches before the tail)
+    const uint32_t n_st = n_in < a->dyn_from ? n_in : a->dyn_from;   // static pieces (batches before the tail)
     if (lane < n_st) {
         SvcSlot &s = s_svc[lane];
         s.base = incl - cnt;
@@ -1053,11 +1074,11 @@ __device__ void svc_load_inline(const SvcArgs &a, uint32_t lane)
         s.tile0 = t0;
         s.batch = lane;
         s.dyn = 0;
-        if (!stop && cnt == 0) svc_complete(a.dev, a.tag, lane);
+        if (!stop && cnt == 0) svc_complete(a->dev, a->tag, lane);
     }
     if (lane == 0) {
         s_svc_loaded = n_st;
-        s_dyn_b = a.dyn_from;
+        s_dyn_b = a->dyn_from;
     }
 }
 
@@ -1065,12 +1086,12 @@ __device__ void svc_load_inline(const SvcArgs &a, uint32_t lane)
 // chunk of the dynamic tail, claimed from the current dynamic batch's device-scope counter;
 // past the last dynamic batch, the stop.  A claim that finds its batch exhausted moves the
 // block on to the next batch (every block leaves every dynamic batch through one such claim).
-__device__ void svc_append_dyn(const SvcArgs &a, uint32_t p)
+__device__ __attribute__((noinline)) void svc_append_dyn(KArgs a, uint32_t p)
 {
-    SvcArea *area = &a.dev->area[a.launch & 1];
+    SvcArea *area = &a->dev->area[a->launch & 1];
     SvcSlot &s = s_svc[p % kSvcRing];
     const SvcSlot &q = s_svc[(p + kSvcRing - 1) % kSvcRing];
-    const uint32_t stop_b = a.n_inline - 1;   // the inline stop
+    const uint32_t stop_b = a->n_inline - 1;   // the inline stop
     s.base = q.base + q.count;
     s.done = 0;
     s.dyn = 1;
@@ -1082,13 +1103,13 @@ __device__ void svc_append_dyn(const SvcArgs &a, uint32_t p)
             s.batch = stop_b;
             break;
         }
-        const SvcDescLite d = a.inl[b];
+        const SvcDescLite d = karg_desc(a, b);
         const uint64_t T = (d.n + 63) / 64;
-        const uint64_t x = __hip_atomic_fetch_add(&area->ctr[b], (uint64_t)a.dyn_chunk, __ATOMIC_RELAXED,
+        const uint64_t x = __hip_atomic_fetch_add(&area->ctr[b], (uint64_t)a->dyn_chunk, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
         if (x < T) {
             s.stop = 0;
-            s.count = (uint32_t)(T - x < a.dyn_chunk ? T - x : a.dyn_chunk);
+            s.count = (uint32_t)(T - x < a->dyn_chunk ? T - x : a->dyn_chunk);
             s.recs = d.recs;
             s.bits = d.bits;
             s.n = d.n;
@@ -1105,14 +1126,14 @@ __device__ void svc_append_dyn(const SvcArgs &a, uint32_t p)
 // The wave has just entered batch b: if batch b + 1 is not loaded yet and nobody is loading,
 // take one look for its descriptor now, so the block's waves find it loaded when they reach
 // the end of batch b instead of waiting there.
-__device__ __forceinline__ void svc_prefetch(const SvcArgs &a, uint32_t lane, uint32_t b)
+__device__ __forceinline__ void svc_prefetch(KArgs a, uint32_t lane, uint32_t b)
 {
     if (lane == 0 && __hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1) {
         uint32_t expect = 0;
         if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
             if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1) {
-                if (b + 1 >= a.dyn_from) svc_append_dyn(a, b + 1);   // claim the next chunk ahead
+                if (b + 1 >= a->dyn_from) svc_append_dyn(a, b + 1);   // claim the next chunk ahead
                 else (void)svc_load(a, b + 1, false);
             }
             __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1122,7 +1143,7 @@ __device__ __forceinline__ void svc_prefetch(const SvcArgs &a, uint32_t lane, ui
 
 // Map block tile number g to its batch (mb: batch of the wave's previous claim, g only
 // grows).  Not blocking: kSvcPending if g lies in a batch the host has not posted yet.
-__device__ __forceinline__ SvcClaim svc_map(const SvcArgs &a, uint32_t lane, uint32_t g, bool blocking, uint32_t &mb,
+__device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, bool blocking, uint32_t &mb,
                                             const SvcTile &hint, SvcTile &t)
 {
     if (g - hint.base < hint.count) {   // same batch as the wave's current tile: no LDS reads
@@ -1164,7 +1185,7 @@ __device__ __forceinline__ SvcClaim svc_map(const SvcArgs &a, uint32_t lane, uin
                                                      __HIP_MEMORY_SCOPE_WORKGROUP)) {
                 r = 1;
                 if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == L) {
-                    if (L >= a.dyn_from) svc_append_dyn(a, L);
+                    if (L >= a->dyn_from) svc_append_dyn(a, L);
                     else if (!svc_load(a, L, blocking)) r = 2;
                 }
                 __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1176,9 +1197,9 @@ __device__ __forceinline__ SvcClaim svc_map(const SvcArgs &a, uint32_t lane, uin
             // watchdog: the loader is bounded by idle_ticks; never wait much longer here
             const uint64_t now = memrealtime();
             if (!t_wait) t_wait = now;
-            if (now - t_wait > 2 * a.idle_ticks + 100000000ull) {
+            if (now - t_wait > 2 * a->idle_ticks + 100000000ull) {
                 if (lane == 0)
-                    __hip_atomic_store(&a.host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&a->host->status, kSvcWatchdog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return kSvcStop;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1187,24 +1208,28 @@ __device__ __forceinline__ SvcClaim svc_map(const SvcArgs &a, uint32_t lane, uin
 }
 
 template <int KEYSEL, int TAB>
-__global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
+__global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
 {
+    // the fields through the kernarg segment pointer (constant address space): no private copy
+    // of the 2.4 KB argument struct, and helpers take the pointer
+    const KArgs a = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
     const uint32_t lane = threadIdx.x & 63;
-    SvcDev *dev = a.dev;
+    SvcDev *dev = a->dev;
     if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_entry[blockIdx.x] = memrealtime();
-    UniformKey ukey(a.tab);
-    const uint32_t inf_off = a.inf_off, hf_off = a.hf_off;
+    UniformKey ukey(a->tab);
+    const uint32_t inf_off = a->inf_off, hf_off = a->hf_off;
     if (threadIdx.x == 0) {
         s_svc_next = 0;
         s_svc_lock = 0;
-        s_svc_tag = a.tag;
-        s_svc_c0 = svc_cum(a.weights, blockIdx.x);
-        s_svc_c1 = svc_cum(a.weights, blockIdx.x + 1);
-        s_svc_w = svc_cum(a.weights, gridDim.x);
+        s_svc_tag = a->tag;
+        s_svc_c0 = karg_cum(a, blockIdx.x);
+        s_svc_c1 = karg_cum(a, blockIdx.x + 1);
+        s_svc_w = karg_cum(a, gridDim.x);
     }
     if (threadIdx.x < 64) svc_load_inline(a, lane);   // the batches posted before the launch
     if (blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + 64) {   // the next grid's scratch
-        SvcArea *nx = &dev->area[(a.launch + 1) & 1];
+        SvcArea *nx = &dev->area[(a->launch + 1) & 1];
         nx->ctr[lane] = 0;
         nx->bdone[lane] = 0;
         if (lane == 0) nx->block_waits = 0;
@@ -1215,14 +1240,14 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
     // starts relaying right after it.
     const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
     const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
-    if (!relay) fill_ttab_dma_issue_n<TAB>(a.ttab_img, threadIdx.x >> 6, nthr >> 6);
+    if (!relay) fill_ttab_dma_issue_n<TAB>(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
-        if (!relay) fill_keys(a.tab, nthr);
+        if (!relay) fill_keys(a->tab, nthr);
     } else if constexpr (KEYSEL == kKeyselGather) {
-        fill_valid(a.tab);
+        fill_valid(a->tab);
     } else if constexpr (KEYSEL == kKeyselSched) {
-        if (!relay) fill_keys3(a.tab, nthr);
+        if (!relay) fill_keys3(a->tab, nthr);
     }
     __syncthreads();
     if (threadIdx.x == 0) dev->blk_start[blockIdx.x] = memrealtime();
@@ -1277,7 +1302,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
             const uint32_t old = __hip_atomic_fetch_add(&s.done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old + k == cnt) {   // the piece is verified
                 if (s.dyn) dyn_done(a, s.batch, cnt);
-                else svc_complete(dev, a.tag, s.batch);
+                else svc_complete(dev, a->tag, s.batch);
             }
         }
     };
@@ -1310,7 +1335,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
         // per-interface keys: this tile's key rows, issued BEFORE the next tile's record loads
         // (vmcnt retires in order: a row wait must not also wait for those HBM loads)
         GatherKey gk;
-        if constexpr (KEYSEL == kKeyselGather) gk.issue(a.tab, rec_key_slot(rc));
+        if constexpr (KEYSEL == kKeyselGather) gk.issue(a->tab, rec_key_slot(rc));
         uint32_t g;
         if constexpr (HFV_SVC_AHEAD) {
             g = wave_uniform(gq);
@@ -1373,7 +1398,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs a)
         cur = nx;
         rc = rn;
     }
-    prof.flush(a.host, lane, prof_t0);
+    prof.flush(a->host, lane, prof_t0);
     if (HFV_SVC_SPAN && lane == 0) dev->span_exit[blockIdx.x * 16 + (threadIdx.x >> 6)] = memrealtime();
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dev->run_clock[2] = __builtin_amdgcn_s_memtime();

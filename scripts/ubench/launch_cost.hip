@@ -21,6 +21,21 @@ __global__ __launch_bounds__(1024) void k_lds(int *p, const int *q, void *a, voi
     if (p && big[(threadIdx.x + 1) & 1023] == 99999u) p[0] = 1;
 }
 
+// the same kernel with a by-value argument struct of N bytes (the service's SvcArgs carries up
+// to kSvcInline = 64 inline descriptors: ~2.3 KiB)
+template <int N>
+struct BigArg {
+    unsigned long w[N / 8];
+};
+template <int N>
+__global__ __launch_bounds__(1024) void k_lds_arg(const BigArg<N> a)
+{
+    __shared__ unsigned big[36864];   // 144 KiB
+    big[threadIdx.x] = (unsigned)a.w[threadIdx.x % (N / 8)];
+    __syncthreads();
+    if (big[(threadIdx.x + 1) & 1023] == 99999u) big[0] = 1;
+}
+
 using clk = std::chrono::steady_clock;
 static double us(clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); }
 
@@ -65,6 +80,18 @@ int main()
     }, s);
     measure("lds144K 256x1024 hipExtLaunchKernel no ev", [&] {
         hipExtLaunchKernelGGL(k_lds, dim3(256), dim3(1024), 0, s, nullptr, nullptr, 0u, nullptr, p, p, p, 1u, 2u, 3ul, 4ul);
+    }, s);
+    BigArg<128> a128 = {};
+    BigArg<1024> a1k = {};
+    BigArg<2304> a2k = {};
+    measure("lds144K struct arg 128 B, no ev", [&] {
+        hipExtLaunchKernelGGL(k_lds_arg<128>, dim3(256), dim3(1024), 0, s, nullptr, nullptr, 0u, a128);
+    }, s);
+    measure("lds144K struct arg 1 KiB, no ev", [&] {
+        hipExtLaunchKernelGGL(k_lds_arg<1024>, dim3(256), dim3(1024), 0, s, nullptr, nullptr, 0u, a1k);
+    }, s);
+    measure("lds144K struct arg 2.25 KiB, no ev", [&] {
+        hipExtLaunchKernelGGL(k_lds_arg<2304>, dim3(256), dim3(1024), 0, s, nullptr, nullptr, 0u, a2k);
     }, s);
     measure("lds144K + hipEventRecord around", [&] {
         (void)hipEventRecord(e0, s);

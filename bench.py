@@ -415,7 +415,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
             if run_async:
                 svc["grid_ms"] = ctx.service_stop()   # reaps the exited grid: its lifetime (0 untimed)
             rs.append((el, per_rank, svc["grid_ms"], ctx.service_shader_mhz(), svc["call_us"],
-                       ctx.service_weights()))   # diagnostics
+                       ctx.service_weights(), ctx.service_relay()))   # diagnostics
             check(steps)
         return rs
 
@@ -426,7 +426,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         runs = truns
     runs.sort(key=lambda r: r[0])
     truns_s = sorted(truns, key=lambda r: r[2])
-    svc_el, per_rank, _, mhz, _, _ = runs[len(runs) // 2]
+    svc_el, per_rank, _, mhz = runs[len(runs) // 2][:4]
     grid_ms = truns_s[len(truns_s) // 2][2]
     out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
                 "svc_all_ms": [round(r[0] * 1e3, 4) for r in runs],
@@ -437,6 +437,13 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
                 # next grid (a slow grid at a normal clock with skewed weights is a balance fault)
                 "svc_grid_mhz": [round(r[3], 1) if r[3] else None for r in truns],
                 "svc_weights": [r[5] for r in truns],
+                # per grid (value regions, then event-timed ones): the host link as the relay saw
+                # it -- a PCIe round trip probed at grid start, descriptors in the kernel arguments /
+                # fetched by the relay, waits of a block for a descriptor (0: no grid ran at the
+                # pace of host round trips, the round-3 driver fault)
+                "svc_relay": [{"probe_rtt_us": r[6]["probe_rtt_us"], "inline": r[6]["inline"],
+                               "relayed": r[6]["relayed"], "block_waits": r[6]["block_waits"]}
+                              for r in list(runs if not timed_value else []) + truns if r[6]],
                 "svc_value_regions": "timed with dispatch events" if timed_value else "no timing events"})
     return out
 
@@ -865,6 +872,10 @@ def run_hf(args, W):
         os.environ["HFV_SVC_GRID"] = str(max(1, cus // W.size))
     m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream, reps=args.svc_reps,
                    service=not args.launch_only)
+    # every rank's median event-timed grid (the service's kernel time per rank), and no rank starts
+    # an extra leg (host threads, PCIe copies) while another is still in its headline regions
+    per_rank_grid = W.gather(m["grid_ms"] or 0.0)
+    W.barrier()
     headline = "launch" if args.launch_only else args.mode
     elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
     bytes_per_batch = BYTES_PER_PACKET * n
@@ -922,6 +933,7 @@ def run_hf(args, W):
             "event_timed_regions_ms": m.get("svc_timed_regions_ms"), "value_regions": m.get("svc_value_regions"),
             "service_run_call_us": m.get("svc_all_call_us"),
             "grids_mhz": m.get("svc_grid_mhz"), "weights": m.get("svc_weights"),
+            "relay": m.get("svc_relay"),
             "note": f"value = the median of {args.svc_reps} timed regions of K steps each (each a fresh grid)"},
         "per_launch": {"mpkts": round(total * args.steps / m["launch_el"] / 1e6, 2),
                        "ms_per_step": round(m["launch_el"] / args.steps * 1e3, 5),
@@ -929,7 +941,8 @@ def run_hf(args, W):
                        "kernel_mpkts": round(n / m["k_mean"] / 1e3, 1),
                        "frac": round(bytes_per_batch / (m["k_mean"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "per_rank_ms": {"min": round(min(m["per_rank_s"]) * 1e3, 4), "max": round(max(m["per_rank_s"]) * 1e3, 4),
-                        "all": [round(x * 1e3, 4) for x in m["per_rank_s"]]},
+                        "all": [round(x * 1e3, 4) for x in m["per_rank_s"]],
+                        "grid_ms": [round(x, 4) for x in per_rank_grid] if headline == "service" else None},
         "host_threads": tb,
     }
     if args.same_device:

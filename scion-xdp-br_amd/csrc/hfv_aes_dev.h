@@ -84,9 +84,17 @@ __device__ __forceinline__ void fill_ttab()
     }
 }
 
-// Same table image copied from a prebuilt global copy (ctx->ttab_img, L2-resident after the
-// first blocks) by LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB per wave-instruction
-// straight into LDS, no VGPR round trip and ~16x fewer instructions than fill_ttab.
+// Same tables copied into LDS by LDS-DMA: one global_load_lds_dwordx4 writes 1 KiB of LDS per
+// wave-instruction, no VGPR round trip and ~16x fewer instructions than fill_ttab.  The source
+// is the compact image (k_build_ttab_image): the 64 lanes of LDS chunk c (8 runs of 32 lane
+// copies) read entries 8c .. 8c + 7, 8 lanes per 16-byte entry, so a block reads 16 KiB from L2
+// instead of the 128 KiB it writes (round 3 copied a 128 KiB replicated image: 4.4-5 us from
+// block entry to the fill barrier, the whole chip pulling 32 MiB through L2 at every grid start).
+__device__ __forceinline__ const char *ttab_src(const uint32_t *img, uint32_t chunk, uint32_t lane)
+{
+    return reinterpret_cast<const char *>(img) + (size_t)((chunk << 3) + (lane >> 3)) * 16;
+}
+
 // Issue-only form with the block size known at compile time (reading blockDim would add a
 // dispatch-packet load whose wait also drains the record loads issued before the fill).
 template <int TAB, int BLOCK>
@@ -97,7 +105,7 @@ __device__ __forceinline__ void fill_ttab_dma_issue(const uint32_t *__restrict__
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
     for (int c = wave; c < kChunks; c += nw) {
-        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        const char *src = ttab_src(img, c, lane);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                          (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
     }
@@ -112,9 +120,103 @@ __device__ __forceinline__ void fill_ttab_dma_issue_n(const uint32_t *__restrict
     const int lane = threadIdx.x & 63;
     char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
     for (uint32_t c = wave; c < kChunks; c += nw) {
-        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        const char *src = ttab_src(img, c, lane);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                          (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
+    }
+}
+
+// The same copy through VGPRs: each filling wave loads its chunks' 16-byte pieces from the
+// compact image (global_load_dwordx4, all issued at once), then writes them with
+// ds_write_b128 (≈79 B/clk/CU).  issue() and commit() are split so a kernel can put other
+// loads (a first tile's records) between them: vmcnt retires in order, so the table pieces,
+// issued first, can be written while those are still in flight.  For 15 or 16 filling waves.
+template <int TAB>
+struct TtabRegs {
+    static constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    static constexpr int kMax = (int)((kChunks + 14) / 15);
+    uint4 v[kMax];
+    __device__ __forceinline__ void issue(const uint32_t *__restrict__ img, uint32_t wave, uint32_t nw)
+    {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < kMax; ++k) {
+            const uint32_t c = wave + k * nw;
+            if (c < kChunks) {
+                typedef const __attribute__((address_space(1))) v4 *G4;
+                const v4 x = *(G4)(ttab_src(img, c, lane));   // global, not flat: vmcnt only
+                v[k] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+        }
+    }
+    __device__ __forceinline__ void commit(uint32_t wave, uint32_t nw) const
+    {
+        const uint32_t lane = threadIdx.x & 63;
+        char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
+#pragma unroll
+        for (int k = 0; k < kMax; ++k) {
+            const uint32_t c = wave + k * nw;
+            if (c < kChunks) *reinterpret_cast<uint4 *>(lds + c * 1024 + lane * 16) = v[k];
+        }
+    }
+};
+
+// The tables computed in the block instead of copied: no memory access at all, so a block's
+// fill does not wait on a cold L2 / HBM at grid start (the copies above took 4.0-4.6 us from
+// block entry to the fill barrier whatever their source size, round 4 span probe).  Threads
+// 0..255 compute T0[x] (S-box by GF(2^8) inversion x^254 and the FIPS-197 affine map, as
+// hfv_tables.h does at compile time) into a 1 KiB staging array; after a barrier every filling
+// lane writes its chunk's 16-byte pieces (4 copies of one table value) with ds_write_b128.
+static __shared__ uint32_t s_t0stage[256];
+
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b)   // GF(2^8), x^8 + x^4 + x^3 + x + 1
+{
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        p ^= a & (0u - ((b >> i) & 1u));
+        a = (a << 1) ^ (0x11bu & (0u - ((a >> 7) & 1u)));
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t t0_calc(uint32_t x)
+{
+    const uint32_t x2 = gf_mul(x, x), x3 = gf_mul(x2, x), x6 = gf_mul(x3, x3), x12 = gf_mul(x6, x6);
+    uint32_t y = gf_mul(x12, x3);   // x^15
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y = gf_mul(y, y);   // x^240
+    const uint32_t inv = gf_mul(gf_mul(y, x12), x2);   // x^254 = x^-1 (0 -> 0)
+    uint32_t sb = inv, r = inv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        r = ((r << 1) | (r >> 7)) & 0xffu;
+        sb ^= r;
+    }
+    sb ^= 0x63u;
+    const uint32_t s2 = ((sb << 1) ^ (0x11bu & (0u - (sb >> 7)))) & 0xffu;
+    return s2 | sb << 8 | sb << 16 | (s2 ^ sb) << 24;
+}
+
+// Phase A (threads 0..255 of the block) -- then a __syncthreads() that every wave of the block
+// reaches -- then phase B (the `nw` filling waves; wave index `wave`).
+__device__ __forceinline__ void fill_ttab_calc_stage()
+{
+    if (threadIdx.x < 256) s_t0stage[threadIdx.x] = t0_calc(threadIdx.x);
+}
+template <int TAB>
+__device__ __forceinline__ void fill_ttab_calc_write(uint32_t wave, uint32_t nw)
+{
+    constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    const uint32_t lane = threadIdx.x & 63;
+    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
+    for (uint32_t c = wave; c < kChunks; c += nw) {
+        const uint32_t e = (c << 3) + (lane >> 3);               // 128-byte run: table t, index x
+        const uint32_t t = (e & 1u) | (((e >> 9) & 1u) << 1);
+        const uint32_t v0 = s_t0stage[(e >> 1) & 255u];
+        const uint32_t v = t ? __builtin_amdgcn_alignbit(v0, v0, 32 - 8 * t) : v0;
+        *reinterpret_cast<uint4 *>(lds + c * 1024 + lane * 16) = make_uint4(v, v, v, v);
     }
 }
 
@@ -125,7 +227,7 @@ __device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
     char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
     for (int c = wave; c < kChunks; c += nw) {
-        const char *src = reinterpret_cast<const char *>(img) + c * 1024 + lane * 16;
+        const char *src = ttab_src(img, c, lane);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                          (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
     }

@@ -443,7 +443,7 @@ int hfv_ctx_create(int device, hfv_ctx **out)
             return fail(-EINVAL, "no kernel variant matches HFV_KVARIANT / HFV_KVARIANT_IFID");
         }
         uint32_t *img = nullptr;
-        if (hipMalloc((void **)&img, 131072) != hipSuccess) { rc = -ENOMEM; break; }
+        if (hipMalloc((void **)&img, kTtabImageDwords * 4) != hipSuccess) { rc = -ENOMEM; break; }
         c->geom.ttab_img = img;
         if (build_ttab_image(img, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess) { rc = -EIO; break; }
     } while (0);

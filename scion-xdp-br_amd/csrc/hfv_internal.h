@@ -186,7 +186,7 @@ struct LaunchGeom {
     int num_cus;
     KernelVariant single;   // KEYSEL_ZERO record verify
     KernelVariant multi;    // KEYSEL_IFID record verify (per-lane keys in LDS)
-    const uint32_t *ttab_img;   // 128 KiB device image of the replicated T0..T3 tables
+    const uint32_t *ttab_img;   // 16 KiB compact source of the replicated T0..T3 LDS tables (k_build_ttab_image)
 };
 
 // kernel launchers (hfv_kernels.hip); return hipError_t as int
@@ -210,6 +210,7 @@ int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, 
 int query_geometry(int device, LaunchGeom *g);
 int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream);
+constexpr uint32_t kTtabImageDwords = 4096;   // 1024 entries x 16 B
 int build_ttab_image(uint32_t *img, void *stream);
 // persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
 // block waits for the next descriptor before it exits with status kSvcIdleTimeout

@@ -29,14 +29,25 @@
 
 namespace hfv {
 
-// Prebuilt LDS image of the round tables (the fill_ttab_dma source), built once per ctx.
+// How a block fills its LDS round tables: 0 computed in the block (fill_ttab_calc_*: no memory
+// access), 1 LDS-DMA from the compact image (round 3's method), 2 copied through VGPRs.
+#ifndef HFV_FILL
+#define HFV_FILL 0
+#endif
+
+// Compact source of the LDS round tables (the fill_ttab_dma source), built once per ctx:
+// 16 KiB, entry e (16 bytes = 4 copies of one table value) for the 128-byte run of LDS
+// (32 lane copies of table t at index x) that starts at byte e * 128 of the LDS image.  Every
+// lane of an LDS-DMA instruction fetches its 16 bytes from entry (LDS offset / 128), so a
+// block moves 16 KiB from L2 instead of a 128 KiB replicated image (ttab_src, hfv_aes_dev.h).
 __global__ void k_build_ttab_image(uint32_t *__restrict__ img)
 {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= 32768) return;
-    uint32_t t = c_t0[(e >> 6) & 255];
-    int rot = 8 * (((e >> 5) & 1) | ((e >> 13) & 2));
-    img[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int)kTtabImageDwords) return;
+    const int e = i >> 2;
+    const uint32_t t0 = c_t0[(e >> 1) & 255];
+    const int t = (e & 1) | (((e >> 9) & 1) << 1);
+    img[i] = t ? __builtin_amdgcn_alignbit(t0, t0, 32 - 8 * t) : t0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -247,12 +258,28 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
     // (Waiting at the barrier only for the table, and for the records after it, needs the
     // record loads pinned ahead of the barrier and the waitcnt pass told that the LDS-DMA
     // writes are done; every form tried made the compiler drain the prefetch each tile.)
-    RecWords cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
-    if constexpr (DMA) {
-        fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RecWords cur;
+    if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 0) {
+        // records first (their HBM latency overlaps the table computation), then the tables
+        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+        fill_ttab_calc_stage();
+        __syncthreads();
+        fill_ttab_calc_write<TAB>(threadIdx.x >> 6, BLOCK / 64);
+    } else if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 2) {
+        // table pieces first, then the first tile's records: the pieces land (in order) and are
+        // written to LDS while the records are still on their way from HBM
+        TtabRegs<TAB> tr;
+        tr.issue(ttab_img, threadIdx.x >> 6, BLOCK / 64);
+        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+        tr.commit(threadIdx.x >> 6, BLOCK / 64);
     } else {
-        fill_ttab<TAB>();
+        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+        if constexpr (DMA) {
+            fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            fill_ttab<TAB>();
+        }
     }
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
     __syncthreads();
@@ -525,7 +552,7 @@ __global__ __launch_bounds__(BLOCK) void k_verify_hybrid(const DevKeyTable *__re
         const int nw = kTT;
         char *ldst = reinterpret_cast<char *>(s_tab64);
         for (int ch = wv; ch < 64; ch += nw) {
-            const char *src = reinterpret_cast<const char *>(ttab_img) + ch * 1024 + lane * 16;
+            const char *src = ttab_src(ttab_img, ch, lane);
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                              (__attribute__((address_space(3))) void *)(ldst + ch * 1024), 16, 0, 0);
         }
@@ -1240,8 +1267,20 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     // starts relaying right after it.
     const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
     const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
+#if HFV_FILL == 1
     if (!relay) fill_ttab_dma_issue_n<TAB>(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif HFV_FILL == 2
+    if (!relay) {
+        TtabRegs<TAB> tr;
+        tr.issue(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
+        tr.commit(threadIdx.x >> 6, nthr >> 6);
+    }
+#else
+    fill_ttab_calc_stage();
+    __syncthreads();
+    if (!relay) fill_ttab_calc_write<TAB>(threadIdx.x >> 6, nthr >> 6);
+#endif
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
         if (!relay) fill_keys(a->tab, nthr);
     } else if constexpr (KEYSEL == kKeyselGather) {
@@ -1826,7 +1865,7 @@ static int finish_variant(int keysel, KernelVariant *v)
 
 int build_ttab_image(uint32_t *img, void *stream)
 {
-    hipLaunchKernelGGL(k_build_ttab_image, dim3(128), dim3(256), 0, (hipStream_t)stream, img);
+    hipLaunchKernelGGL(k_build_ttab_image, dim3(kTtabImageDwords / 256), dim3(256), 0, (hipStream_t)stream, img);
     return (int)hipGetLastError();
 }
 

@@ -59,6 +59,14 @@ def test_two_service_ranks_on_one_gpu():
     assert d["roofline"]["kernel"] == "k_verify_service" and d["value"] > 0
     assert int(d["same_device"]["service_grid_blocks"]) * 2 <= 256
     assert d["host_threads"]["ranks_on_node"] == 2 and d["host_threads"]["budget"] >= 1   # OMP_NUM_THREADS=1 here
+    # per-rank grid times.  Each rank's grid verifies 8 x 2^18 records on half the
+    # CUs side by side with the other's: about as long as one full-chip grid over 8 x 2^19
+    # (~0.1 ms at 0.7 of 8 TB/s); neither rank's grid runs at the pace of host round trips (the
+    # round-3 fault: ~40 us per batch) and the two stay within 1.5x of each other.
+    g = d["per_rank_ms"]["grid_ms"]
+    assert len(g) == 2 and all(0 < x < 0.3 for x in g), g
+    assert max(g) < 1.5 * min(g), g
+    assert all(r["block_waits"] == 0 for r in d["service"]["relay"]), d["service"]["relay"]
 
 
 @pytest.mark.gpu

@@ -162,61 +162,32 @@ struct TtabRegs {
     }
 };
 
-// The tables computed in the block instead of copied: no memory access at all, so a block's
-// fill does not wait on a cold L2 / HBM at grid start (the copies above took 4.0-4.6 us from
-// block entry to the fill barrier whatever their source size, round 4 span probe).  Threads
-// 0..255 compute T0[x] (S-box by GF(2^8) inversion x^254 and the FIPS-197 affine map, as
-// hfv_tables.h does at compile time) into a 1 KiB staging array; after a barrier every filling
-// lane writes its chunk's 16-byte pieces (4 copies of one table value) with ds_write_b128.
-static __shared__ uint32_t s_t0stage[256];
-
-__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b)   // GF(2^8), x^8 + x^4 + x^3 + x + 1
-{
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        p ^= a & (0u - ((b >> i) & 1u));
-        a = (a << 1) ^ (0x11bu & (0u - ((a >> 7) & 1u)));
-    }
-    return p;
-}
-
-__device__ __forceinline__ uint32_t t0_calc(uint32_t x)
-{
-    const uint32_t x2 = gf_mul(x, x), x3 = gf_mul(x2, x), x6 = gf_mul(x3, x3), x12 = gf_mul(x6, x6);
-    uint32_t y = gf_mul(x12, x3);   // x^15
-#pragma unroll
-    for (int i = 0; i < 4; ++i) y = gf_mul(y, y);   // x^240
-    const uint32_t inv = gf_mul(gf_mul(y, x12), x2);   // x^254 = x^-1 (0 -> 0)
-    uint32_t sb = inv, r = inv;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        r = ((r << 1) | (r >> 7)) & 0xffu;
-        sb ^= r;
-    }
-    sb ^= 0x63u;
-    const uint32_t s2 = ((sb << 1) ^ (0x11bu & (0u - (sb >> 7)))) & 0xffu;
-    return s2 | sb << 8 | sb << 16 | (s2 ^ sb) << 24;
-}
-
-// Phase A (threads 0..255 of the block) -- then a __syncthreads() that every wave of the block
-// reaches -- then phase B (the `nw` filling waves; wave index `wave`).
-__device__ __forceinline__ void fill_ttab_calc_stage()
-{
-    if (threadIdx.x < 256) s_t0stage[threadIdx.x] = t0_calc(threadIdx.x);
-}
-template <int TAB>
-__device__ __forceinline__ void fill_ttab_calc_write(uint32_t wave, uint32_t nw)
+// The tables written from T0 in the kernel arguments (constant address space, one memory hop
+// with the rest of the arguments): every filling lane loads T0 of its chunks' runs and writes
+// 16-byte pieces (4 copies of the table value) with ds_write_b128.
+template <int TAB, class P>
+__device__ __forceinline__ void fill_ttab_karg(P t0, uint32_t wave, uint32_t nw)
 {
     constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
+    constexpr int kMax = (int)((kChunks + 14) / 15);   // at least 15 filling waves
     const uint32_t lane = threadIdx.x & 63;
     char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-    for (uint32_t c = wave; c < kChunks; c += nw) {
-        const uint32_t e = (c << 3) + (lane >> 3);               // 128-byte run: table t, index x
-        const uint32_t t = (e & 1u) | (((e >> 9) & 1u) << 1);
-        const uint32_t v0 = s_t0stage[(e >> 1) & 255u];
-        const uint32_t v = t ? __builtin_amdgcn_alignbit(v0, v0, 32 - 8 * t) : v0;
-        *reinterpret_cast<uint4 *>(lds + c * 1024 + lane * 16) = make_uint4(v, v, v, v);
+    uint32_t v[kMax];
+#pragma unroll
+    for (int k = 0; k < kMax; ++k) {
+        const uint32_t c = wave + k * nw;
+        const uint32_t e = (c << 3) + (lane >> 3);   // 128-byte run of table t at index x
+        v[k] = c < kChunks ? t0[(e >> 1) & 255u] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kMax; ++k) {
+        const uint32_t c = wave + k * nw;
+        if (c < kChunks) {
+            const uint32_t e = (c << 3) + (lane >> 3);
+            const uint32_t t = (e & 1u) | (((e >> 9) & 1u) << 1);
+            const uint32_t x = t ? __builtin_amdgcn_alignbit(v[k], v[k], 32 - 8 * t) : v[k];
+            *reinterpret_cast<uint4 *>(lds + c * 1024 + lane * 16) = make_uint4(x, x, x, x);
+        }
     }
 }
 
@@ -373,6 +344,16 @@ struct UniformKey {          // slot 0 for every lane, kept in SGPRs
             k[r] = make_uint4(p[0], p[1], p[2], p[3]);
         }
         ok = tab->valid[0] & 1u;
+    }
+    // the rows from the kernel arguments (constant address space: scalar loads); P is the
+    // kernarg pointer type (address space 4, or generic into a by-value kernel argument, which
+    // the compiler keeps in the kernarg segment)
+    template <class P>
+    __device__ __forceinline__ UniformKey(P rows, uint32_t valid)
+    {
+#pragma unroll
+        for (int r = 0; r < kDevKeyRows; ++r) k[r] = make_uint4(rows[4 * r], rows[4 * r + 1], rows[4 * r + 2], rows[4 * r + 3]);
+        ok = valid & 1u;
     }
     __device__ __forceinline__ uint4 row(int r) const { return k[r]; }
     template <int TAB>

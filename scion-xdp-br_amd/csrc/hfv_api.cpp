@@ -652,7 +652,7 @@ int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
     const DevKeyTable *tab = &ds->keys;
-    int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
+    int e = launch_verify_records(ctx->geom, tab, &ctx->host_img->keys, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
                                   ctx->hf_off, pass_bits, st);
     return after_launch(ctx, st, e, "verify_records launch");
 }
@@ -677,7 +677,7 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
     const DevKeyTable *tab = &ds->keys;
-    int e = launch_verify_records(ctx->geom, tab, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
+    int e = launch_verify_records(ctx->geom, tab, &ctx->host_img->keys, ctx->keysel, (const uint8_t *)recs, stride, n, ctx->inf_off,
                                   ctx->hf_off, pass_bits, st, ctx->tev[0], ctx->tev[1]);
     rc = after_launch(ctx, st, e, "verify_records launch");
     if (rc) return rc;
@@ -702,7 +702,7 @@ extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n
     const DevKeyTable *tab = &ds->keys;
     uint64_t tiles = (n + 63) / 64, blocks = (tiles + 15) / 16, cap = (uint64_t)ctx->geom.num_cus * ctx->geom.single.blocks_per_cu;
     *grid = (int)(blocks < cap ? blocks : cap);
-    int e = launch_verify_stamped(ctx->geom, tab, (const uint8_t *)recs, n, pass_bits, stamps, st);
+    int e = launch_verify_stamped(ctx->geom, tab, &ctx->host_img->keys, (const uint8_t *)recs, n, pass_bits, stamps, st);
     return after_launch(ctx, st, e, "stamped launch");
 }
 
@@ -1418,7 +1418,7 @@ static int verify_records_zero_copy(hfv_ctx *ctx, const uint8_t *drecs, size_t s
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_verify_records(ctx->geom, &ds->keys, ctx->keysel, drecs, stride, n, ctx->inf_off, ctx->hf_off,
+    int e = launch_verify_records(ctx->geom, &ds->keys, &ctx->host_img->keys, ctx->keysel, drecs, stride, n, ctx->inf_off, ctx->hf_off,
                                   dbits, st, nullptr, nullptr, /*interleaved=*/true);
     rc = after_launch(ctx, st, e, "verify_records launch (zero-copy)");
     if (rc) return rc;
@@ -1481,7 +1481,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
         int rc = publish_keys(ctx, st, &ds);
         if (rc) return rc;
         const DevKeyTable *tab = &ds->keys;
-        int e = launch_verify_records(ctx->geom, tab, ctx->keysel, ctx->d_rec[slot], kHostRec, cnt, 0, 8,
+        int e = launch_verify_records(ctx->geom, tab, &ctx->host_img->keys, ctx->keysel, ctx->d_rec[slot], kHostRec, cnt, 0, 8,
                                       ctx->d_bits[slot], st);
         rc = after_launch(ctx, st, e, "verify_records launch");
         if (rc) return rc;
@@ -1807,6 +1807,11 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     }
     a.relay_delay_us = g_svc_relay_delay_us;
     a.launch = ctx->svc_launches;
+    // slot 0's device key rows as published for this grid (the host image is what the last
+    // publish copied into the device table), and T0
+    for (int r = 0; r < kDevKeyRows; ++r) memcpy(&a.key0[4 * r], ctx->host_img->keys.rows[r][0], 16);
+    a.key0_ok = ctx->host_img->keys.valid[0] & 1u;
+    memcpy(a.t0, kTables.t0, sizeof a.t0);
     // Dynamic tail: in a run whose stop is inline, the last 1-2 batches (K >= 3 / K >= 6) are
     // claimed in chunks instead of fixed shares, so that blocks which got through their shares
     // early take more of them (the grid's blocks otherwise finished 11-17 us apart on a 0.24 ms

@@ -193,7 +193,16 @@ struct LaunchGeom {
 // interleaved: grid-stride tile order (wave w takes tiles w, w + W, ...) instead of one
 // contiguous tile range per block -- for records in host memory, where the 256 ranges far
 // apart thrash the GPU's translation of 4 KiB host pages (zero-copy 2^20: 1.60 -> 1.27 ms)
-int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
+// One-launch-per-batch record verify: the slot-0 key rows and T0 travel in the kernel arguments
+// too (RecArgs), so a block's prologue is one memory hop (SvcArgs has the same fields).
+struct RecArgs {
+    uint32_t key0[kDevKeyRows * 4];
+    uint32_t key0_ok, pad_[3];
+    uint32_t t0[256];
+};
+// host_keys: the key table as last published (the host staging image), for RecArgs
+int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, int keysel,
+                          const uint8_t *recs,
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits,
                           void *stream, void *ev_start = nullptr, void *ev_stop = nullptr,
                           bool interleaved = false);
@@ -208,7 +217,8 @@ int launch_count_verdicts(const LaunchGeom &g, const uint8_t *recs, size_t strid
 int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, uint8_t *recs, size_t stride,
                        size_t n, uint64_t seed, uint64_t first_index, void *stream);
 int query_geometry(int device, LaunchGeom *g);
-int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
+int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, const uint8_t *recs,
+                          size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream);
 constexpr uint32_t kTtabImageDwords = 4096;   // 1024 entries x 16 B
 int build_ttab_image(uint32_t *img, void *stream);
@@ -259,6 +269,12 @@ struct SvcArgs {
     // device-scope counter per batch, so the blocks that finished their earlier shares first
     // take more of the tail and the grid's blocks finish together.  ~0u: none.
     uint32_t dyn_from, dyn_chunk, pad_;
+    // What every block reads before its first tile, in the kernel arguments so that the block
+    // prologue is one memory hop (the kernarg segment) instead of two (kernarg -> key table /
+    // table image): the slot-0 device key rows (KEYSEL_ZERO, as published for this grid) and T0.
+    uint32_t key0[kDevKeyRows * 4];
+    uint32_t key0_ok, pad2_[3];
+    uint32_t t0[256];
     SvcDescLite inl[kSvcInline];
 };
 int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,

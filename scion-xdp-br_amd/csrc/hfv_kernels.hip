@@ -29,10 +29,23 @@
 
 namespace hfv {
 
-// How a block fills its LDS round tables: 0 computed in the block (fill_ttab_calc_*: no memory
-// access), 1 LDS-DMA from the compact image (round 3's method), 2 copied through VGPRs.
+// How the one-launch-per-batch kernel fills its LDS round tables: 3 (default) from T0 in its
+// kernel arguments (RecArgs: the block prologue is one memory hop, the kernarg segment, with the
+// slot-0 key rows alongside); 2 the compact image copied through VGPRs, its pieces issued
+// before the first tile's records (TtabRegs); 1 LDS-DMA from the compact image after the
+// records.  The resident service takes T0 and the key rows from its arguments too
+// (HFV_SVC_FILL_DMA=1: LDS-DMA).  Measured round 4 (profiles/r04/fill_ab.log, span probe):
+// the service's block prologue (entry -> fill barrier) took 4.1-4.5 us with the key rows and
+// the LDS-DMA source behind a second hop (the 16 KiB compact image or round 3's 128 KiB: the
+// same), 3.4 us with the keys in the arguments and LDS-DMA, 3.0 us with both in the arguments;
+// 5.3 us with the tables computed in the block (GF(2^8) inversion in VALU; removed).
 #ifndef HFV_FILL
-#define HFV_FILL 0
+#define HFV_FILL 3
+#endif
+// HFV_SVC_FILL_DMA = 1: the service fills its tables by LDS-DMA from the compact image (a second
+// memory hop after the kernel arguments) instead of from T0 in its kernel arguments
+#ifndef HFV_SVC_FILL_DMA
+#define HFV_SVC_FILL_DMA 0
 #endif
 
 // Compact source of the LDS round tables (the fill_ttab_dma source), built once per ctx:
@@ -241,7 +254,7 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
                                                const uint32_t *__restrict__ ttab_img,
                                                const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
                                                uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
-                                               uint64_t *__restrict__ st)
+                                               uint64_t *__restrict__ st, const RecArgs &ka)
 {
     const uint64_t ntiles = (n + 63) / 64;
     const uint32_t lane = threadIdx.x & 63;
@@ -251,7 +264,7 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
     const uint32_t kWaves = BLOCK / 64;
     // first tile of each wave is static (wave index); the queue hands out the rest
     uint32_t t = wave_uniform(threadIdx.x / 64);
-    UniformKey ukey(tab);
+    UniformKey ukey(ka.key0, ka.key0_ok);   // from the kernel arguments: no second memory hop
     if (threadIdx.x == 0) s_next_tile = kWaves;
     // The wave's first records and its share of the table pieces are in flight together;
     // one vmcnt(0) then covers both (the table must be complete before the barrier).
@@ -259,12 +272,10 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
     // record loads pinned ahead of the barrier and the waitcnt pass told that the LDS-DMA
     // writes are done; every form tried made the compiler drain the prefetch each tile.)
     RecWords cur;
-    if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 0) {
-        // records first (their HBM latency overlaps the table computation), then the tables
+    if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 3) {
+        // the first tile's records, then the tables from T0 in the kernel arguments
         cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
-        fill_ttab_calc_stage();
-        __syncthreads();
-        fill_ttab_calc_write<TAB>(threadIdx.x >> 6, BLOCK / 64);
+        fill_ttab_karg<TAB>(ka.t0, threadIdx.x >> 6, BLOCK / 64);
     } else if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 2) {
         // table pieces first, then the first tile's records: the pieces land (in order) and are
         // written to LDS while the records are still on their way from HBM
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(BLOCK) void k_verify_bs(const DevKeyTable *__restri
                                                      const uint32_t *__restrict__ ttab_img,
                                                      const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
                                                      uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
-                                                     uint64_t *__restrict__ stamps)
+                                                     uint64_t *__restrict__ stamps, const RecArgs ka)
 {
     static_assert(BLOCK / 64 <= (int)kBsMaxWaves, "LDS staging regions");
     const uint32_t lane = threadIdx.x & 63, wv = wave_uniform(threadIdx.x / 64);
@@ -507,7 +518,8 @@ __global__ __launch_bounds__(BLOCK) void k_verify_hybrid(const DevKeyTable *__re
                                                          const uint32_t *__restrict__ ttab_img,
                                                          const uint8_t *__restrict__ recs, uint64_t stride,
                                                          uint64_t n, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps)
+                                                         uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps,
+                                                         const RecArgs ka)
 {
     static_assert(NBS >= 1 && NBS <= (int)kBsMaxWaves && NBS < BLOCK / 64, "wave roles");
     constexpr uint32_t kWaves = BLOCK / 64, kTT = kWaves - NBS;
@@ -581,7 +593,8 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
                                                           const uint32_t *__restrict__ ttab_img,
                                                           const uint8_t *__restrict__ recs, uint64_t stride,
                                                           uint64_t n, uint32_t inf_off, uint32_t hf_off,
-                                                          uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps)
+                                                          uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps,
+                                                          const RecArgs ka)
 {
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     static_assert(NP == 1 || NP == 2, "packets per lane");
@@ -598,7 +611,7 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
     }
 
     if constexpr (DYN) {
-        verify_dynamic<KEYSEL, BLOCK, TAB, DMA, STAMP>(tab, ttab_img, recs, stride, n, inf_off, hf_off, bits, st);
+        verify_dynamic<KEYSEL, BLOCK, TAB, DMA, STAMP>(tab, ttab_img, recs, stride, n, inf_off, hf_off, bits, st, ka);
         return;
     }
     // First tiles' record loads go out before the table fill so the fill overlaps their
@@ -1244,7 +1257,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     const uint32_t lane = threadIdx.x & 63;
     SvcDev *dev = a->dev;
     if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_entry[blockIdx.x] = memrealtime();
-    UniformKey ukey(a->tab);
+    UniformKey ukey(a->key0, a->key0_ok);
     const uint32_t inf_off = a->inf_off, hf_off = a->hf_off;
     if (threadIdx.x == 0) {
         s_svc_next = 0;
@@ -1267,19 +1280,11 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     // starts relaying right after it.
     const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
     const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
-#if HFV_FILL == 1
+#if HFV_SVC_FILL_DMA
     if (!relay) fill_ttab_dma_issue_n<TAB>(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#elif HFV_FILL == 2
-    if (!relay) {
-        TtabRegs<TAB> tr;
-        tr.issue(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
-        tr.commit(threadIdx.x >> 6, nthr >> 6);
-    }
 #else
-    fill_ttab_calc_stage();
-    __syncthreads();
-    if (!relay) fill_ttab_calc_write<TAB>(threadIdx.x >> 6, nthr >> 6);
+    if (!relay) fill_ttab_karg<TAB>(a->t0, threadIdx.x >> 6, nthr >> 6);
 #endif
     if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
         if (!relay) fill_keys(a->tab, nthr);
@@ -1683,7 +1688,19 @@ static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
 }
 
 using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8_t *, uint64_t, uint64_t, uint32_t,
-                              uint32_t, uint64_t *, uint64_t *);
+                              uint32_t, uint64_t *, uint64_t *, const RecArgs);
+
+static RecArgs rec_args(const DevKeyTable *host_keys)
+{
+    RecArgs ka;
+    memset(&ka, 0, sizeof ka);
+    if (host_keys) {
+        for (int r = 0; r < kDevKeyRows; ++r) memcpy(&ka.key0[4 * r], host_keys->rows[r][0], 16);
+        ka.key0_ok = host_keys->valid[0] & 1u;
+    }
+    memcpy(ka.t0, kTables.t0, sizeof ka.t0);
+    return ka;
+}
 
 // Record-verify variants (tuning knobs; the default is chosen by scripts/sweep.py data).
 template <int KEYSEL>
@@ -1716,7 +1733,8 @@ static VerifyKernel pick_verify(const KernelVariant &v)
     return nullptr;
 }
 
-int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, const uint8_t *recs,
+int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, int keysel,
+                          const uint8_t *recs,
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream,
                           void *ev_start, void *ev_stop, bool interleaved)
 {
@@ -1727,20 +1745,23 @@ int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, int keyse
     unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(v.block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)stride,
-                          (uint64_t)n, inf_off, hf_off, bits, (uint64_t *)nullptr);
+                          (uint64_t)n, inf_off, hf_off, bits, (uint64_t *)nullptr, rec_args(host_keys));
     return (int)hipGetLastError();
 }
 
-int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const uint8_t *recs, size_t n,
+int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, const uint8_t *recs,
+                          size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream)
 {
     const KernelVariant &v = g.single;
     unsigned grid = grid_for(n, 1024, g.num_cus, v.blocks_per_cu);
-    auto k = v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 1>
-                   : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 0>;
+    auto k = v.tab == 4 ? (v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 4, 1, 1, 1, 1>
+                                 : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 4, 1, 1, 1, 0>)
+                        : (v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 1>
+                                 : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 0>);
     hipLaunchKernelGGL(k, dim3(grid), dim3(1024), 0,
                        (hipStream_t)stream, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)64, (uint64_t)n,
-                       (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits, stamps);
+                       (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits, stamps, rec_args(host_keys));
     return (int)hipGetLastError();
 }
 

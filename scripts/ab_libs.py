@@ -33,7 +33,8 @@ def main():
             d = json.loads(line[0])
             s = d["service"] or {}
             print(f"{r} {os.path.basename(lib) + ('@' + envs if envs else ''):32s} value {d['value']:9.1f} grid_ms {s.get('grid_ms')} "
-                  f"mhz {s.get('shader_mhz')} launch {d['per_launch']['mpkts']:9.1f}", flush=True)
+                  f"mhz {s.get('shader_mhz')} launch {d['per_launch']['mpkts']:9.1f} "
+                  f"launch_kernel_us {d['per_launch']['kernel_ms_mean'] * 1e3:6.2f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -236,7 +236,6 @@ struct hfv_ctx {
     SvcShared *svc_host_dev = nullptr;
     SvcDev *svc_dev = nullptr;       // device side: relayed descriptors, block completions, diagnostics
     uint32_t svc_launches = 0;       // grids launched (SvcArea parity)
-    uint32_t svc_dyn_from = ~0u;     // the running / last grid's first dynamic batch (SvcArgs::dyn_from)
     unsigned svc_grid = 0;           // blocks of the running grid (each reports its share)
     uint64_t svc_next = 1;           // next grid-local batch number (1, 2, ... per grid)
     uint64_t svc_base = 1;           // ticket of the running grid's batch 1 (tickets are monotonic per ctx)
@@ -1521,7 +1520,6 @@ static bool svc_exited_clean(const hfv_ctx *ctx)
 // watchdog exit, when the relay may not have forwarded everything).
 static bool svc_dev_done(const hfv_ctx *ctx, const std::vector<uint64_t> &done, uint64_t t)
 {
-    if (done[(size_t)kSvcRing * kSvcMaxBlocks + (t - 1) % kSvcRing] >= (ctx->svc_tag | t)) return true;   // bfin
     const uint64_t *d = &done[((t - 1) % kSvcRing) * kSvcMaxBlocks];
     for (unsigned k = 0; k < ctx->svc_grid; ++k)
         if (d[k] < (ctx->svc_tag | t)) return false;
@@ -1540,14 +1538,11 @@ static int svc_dev_read(hfv_ctx *ctx, void *dst, size_t off, size_t bytes)
     return 0;
 }
 
-// SvcDev::done and SvcDev::bfin (adjacent: done first) into one host vector for svc_dev_done.
+// SvcDev::done into a host vector for svc_dev_done.
 static int svc_read_done(hfv_ctx *ctx, std::vector<uint64_t> &done)
 {
-    static_assert(offsetof(SvcDev, done) == offsetof(SvcDev, bfin) + kSvcRing * 8, "layout");
-    done.assign((size_t)kSvcRing * kSvcMaxBlocks + kSvcRing, 0);
-    int rc = svc_dev_read(ctx, done.data(), offsetof(SvcDev, done), (size_t)kSvcRing * kSvcMaxBlocks * 8);
-    if (!rc) rc = svc_dev_read(ctx, done.data() + (size_t)kSvcRing * kSvcMaxBlocks, offsetof(SvcDev, bfin), kSvcRing * 8);
-    return rc;
+    done.assign((size_t)kSvcRing * kSvcMaxBlocks, 0);
+    return svc_dev_read(ctx, done.data(), offsetof(SvcDev, done), done.size() * 8);
 }
 
 static int svc_wait_done(hfv_ctx *ctx, uint64_t t, int timeout_ms)
@@ -1620,12 +1615,9 @@ static void svc_balance(hfv_ctx *ctx)
     for (uint64_t k = 0; k < G; ++k) cum[k + 1] = cum[k] + (k ? wu.w[k % 8] : wu.w0);
     const uint64_t W = cum[G];
     std::vector<double> tiles(G, 0.0);
-    // the static shares only (a dynamic tail's chunks went to whichever block claimed them;
-    // blk_fin is the end of the block's static shares)
-    const size_t nst = std::min(ctx->svc_run_ns.size(), (size_t)ctx->svc_dyn_from);
-    for (size_t i = 0; i < nst;) {   // runs of equal batch sizes at once
+    for (size_t i = 0; i < ctx->svc_run_ns.size();) {   // runs of equal batch sizes at once
         size_t j = i;
-        while (j < nst && ctx->svc_run_ns[j] == ctx->svc_run_ns[i]) ++j;
+        while (j < ctx->svc_run_ns.size() && ctx->svc_run_ns[j] == ctx->svc_run_ns[i]) ++j;
         const uint64_t T = (ctx->svc_run_ns[i] + 63) / 64;
         for (uint64_t k = 0; k < G; ++k)
             tiles[k] += (double)(j - i) * (double)(T * cum[k + 1] / W - T * cum[k] / W);
@@ -1812,25 +1804,6 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     for (int r = 0; r < kDevKeyRows; ++r) memcpy(&a.key0[4 * r], ctx->host_img->keys.rows[r][0], 16);
     a.key0_ok = ctx->host_img->keys.valid[0] & 1u;
     memcpy(a.t0, kTables.t0, sizeof a.t0);
-    // Dynamic tail: in a run whose stop is inline, the last 1-2 batches (K >= 3 / K >= 6) are
-    // claimed in chunks instead of fixed shares, so that blocks which got through their shares
-    // early take more of them (the grid's blocks otherwise finished 11-17 us apart on a 0.24 ms
-    // grid).  HFV_SVC_DYN=0 turns it off (A/B).
-    static const bool dyn_off = getenv("HFV_SVC_DYN") && !strcmp(getenv("HFV_SVC_DYN"), "0");
-    a.dyn_from = ~0u;
-    a.dyn_chunk = 0;
-    const uint32_t K = a.n_inline ? a.n_inline - 1 : 0;
-    if (!dyn_off && a.n_inline && a.inl[K].n == kSvcStopN && K >= 3) {
-        const uint32_t ndyn = K >= 6 ? 2 : 1;
-        uint64_t tmin = ~0ull;
-        for (uint32_t b = K - ndyn; b < K; ++b) tmin = std::min<uint64_t>(tmin, (a.inl[b].n + 63) / 64);
-        const uint64_t G = (uint64_t)ctx->geom.num_cus;
-        if (tmin >= 8 * G) {   // at least one 8-tile chunk per block
-            a.dyn_from = K - ndyn;
-            a.dyn_chunk = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(8, tmin / (2 * G)));
-        }
-    }
-    ctx->svc_dyn_from = a.dyn_from;
     int e = launch_verify_service(ctx->geom, ctx->keysel, a, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0],
                                   noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");

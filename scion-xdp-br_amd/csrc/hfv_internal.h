@@ -142,8 +142,6 @@ enum SvcRelayStat {
 // zeroes area[(L + 1) & 1] for the next grid on the same stream, so no memset op has to run
 // between the host's post and the grid.
 struct SvcArea {
-    uint64_t ctr[kSvcInline];     // dynamic batches: tiles claimed so far (chunk claims)
-    uint32_t bdone[kSvcInline];   // dynamic batches: tiles verified so far
     uint64_t block_waits;         // kRelayBlockWaits
     uint64_t pad[7];
 };
@@ -163,7 +161,6 @@ struct SvcDev {   // device memory: written by the grid; the host copies what it
     uint64_t span_fill[kSvcMaxBlocks];
     uint64_t span_exit[kSvcMaxBlocks * 16];
     SvcArea area[2];
-    uint64_t bfin[kSvcRing];                  // tag | t: dynamic batch t verified (all blocks' pieces)
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
@@ -264,11 +261,7 @@ struct SvcArgs {
     uint32_t n_inline;        // descriptors in inl[] (batches 0 .. n_inline - 1; may end with a stop)
     uint32_t relay_delay_us;  // test hook (hfv_debug_relay_delay): the relay spins this long after each host read
     uint32_t launch;          // grid number (SvcArea parity)
-    // Dynamic tail (inline runs that end with their stop): batches dyn_from .. n_inline - 2 are
-    // not split into fixed per-block shares; blocks claim chunks of dyn_chunk tiles from a
-    // device-scope counter per batch, so the blocks that finished their earlier shares first
-    // take more of the tail and the grid's blocks finish together.  ~0u: none.
-    uint32_t dyn_from, dyn_chunk, pad_;
+    uint32_t pad_[3];
     // What every block reads before its first tile, in the kernel arguments so that the block
     // prologue is one memory hop (the kernarg segment) instead of two (kernarg -> key table /
     // table image): the slot-0 device key rows (KEYSEL_ZERO, as published for this grid) and T0.

@@ -695,13 +695,14 @@ __global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__r
 // overlaps the start of batch b + 1, and the table fill is paid once per service instead of
 // once per batch.
 //
-// Pieces: the block's tile numbers are cut into pieces, s_svc[p % kSvcRing] for piece p.  A
-// static batch b is ONE piece, p = b (the block's share of it); the dynamic tail of an inline
-// run (SvcArgs::dyn_from) is a sequence of pieces, one per chunk the block claimed from a
-// batch's device-scope counter.  The host posts ticket t = b + 1 only after ticket t - kSvcRing
-// completed, so when a block loads batch L every batch up to L - kSvcRing is verified; an
-// unverified claim g therefore lies in one of the newest kSvcRing pieces and never in the slot
-// being overwritten (dynamic pieces are at least 8 tiles: 16 waves hold at most 48 tiles).
+// Descriptor cache: batch b sits in s_svc[b % kSvcRing].  The host posts ticket t = b + 1
+// only after ticket t - kSvcRing completed, so when a block loads batch L every batch up to
+// L - kSvcRing is verified; an unverified claim g therefore lies in one of the newest
+// kSvcRing batches and never in the slot being overwritten.  (Round 4 measured a dynamic tail:
+// the last 1-2 batches of a run claimed in chunks from device-scope counters instead of fixed
+// shares.  Chunks of 32 tiles: -0.5 % grid time, within noise; chunks of 8 from per-XCD
+// counters: +11 %, a claim's round trip is as long as the chunk.  Removed;
+// profiles/ab_index.md.)
 //
 // Completion: verdict words are written through (system-scope stores); a wave counts its
 // verified tiles in the slot's LDS counter once those stores are acknowledged (vmcnt(0)),
@@ -731,13 +732,12 @@ __device__ __forceinline__ uint64_t karg_cum(KArgs a, uint64_t k)
 
 struct SvcSlot {
     uint32_t base, count;   // block tile numbers [base, base + count)
-    uint32_t done, stop;    // tiles of the piece this block has verified; 1: exit descriptor
-    uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the piece
-    uint32_t batch, dyn;    // the piece's batch; 1: a chunk of a dynamic batch
+    uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
+    uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the block's range
+    uint64_t pad;
 };
 static __shared__ SvcSlot s_svc[kSvcRing];
 static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
-static __shared__ uint32_t s_dyn_b;   // the dynamic batch this block claims chunks from
 // Generation tag of this service grid (kernel argument, gen << 40): the host ring, the device
 // mirror and the completion words carry tag | ticket, so words a previous grid left behind
 // never match and nothing has to be cleared between grids.
@@ -852,18 +852,6 @@ __device__ __attribute__((noinline)) void svc_complete(SvcDev *dev, uint64_t tag
     dev->blk_fin[blockIdx.x] = __builtin_amdgcn_s_memrealtime();   // read by the host after the grid
     __hip_atomic_store(&dev->done[b % kSvcRing][blockIdx.x], tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// A piece of dynamic batch b is verified (one lane): the batch's verified-tile count; the
-// block whose piece completes it publishes the batch (dev->bfin).
-__device__ __attribute__((noinline)) void dyn_done(KArgs a, uint32_t b, uint32_t k)
-{
-    SvcArea *area = &a->dev->area[a->launch & 1];
-    const uint32_t T = (uint32_t)((a->inl[b].n + 63) / 64);
-    const uint32_t old = __hip_atomic_fetch_add(&area->bdone[b], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + k == T)
-        __hip_atomic_store(&a->dev->bfin[b % kSvcRing], a->tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ uint64_t memrealtime() { return __builtin_amdgcn_s_memrealtime(); }
@@ -988,9 +976,7 @@ __device__ __attribute__((noinline)) void svc_relay(KArgs a, uint32_t lane, uint
             bool ok = true;
             for (uint32_t k = lane; k < G; k += 64)
                 ok = ok && __hip_atomic_load(&dev->done[f % kSvcRing][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
-            if (__ballot(!ok) &&
-                __hip_atomic_load(&dev->bfin[f % kSvcRing], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
-                break;
+            if (__ballot(!ok)) break;
             if (lane == 0) __hip_atomic_store(&host->done[f % kSvcRing], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             ++f;
             ++fwd;
@@ -1046,8 +1032,6 @@ __device__ __attribute__((noinline)) bool svc_load(KArgs a, uint32_t b, bool blo
     const SvcSlot &p = s_svc[(b + kSvcRing - 1) % kSvcRing];
     s.base = b ? p.base + p.count : 0u;
     s.done = 0;
-    s.batch = b;
-    s.dyn = 0;
     uint64_t n = 0;
     if (!stop) {
         s.recs = __hip_atomic_load(&d->recs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1100,8 +1084,7 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
         const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
         if ((int)lane >= o) incl += y;
     }
-    const uint32_t n_st = n_in < a->dyn_from ? n_in : a->dyn_from;   // static pieces (batches before the tail)
-    if (lane < n_st) {
+    if (lane < n_in) {
         SvcSlot &s = s_svc[lane];
         s.base = incl - cnt;
         s.count = cnt;
@@ -1112,55 +1095,9 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
         s.n = d.n;
         s.stride = d.stride;
         s.tile0 = t0;
-        s.batch = lane;
-        s.dyn = 0;
         if (!stop && cnt == 0) svc_complete(a->dev, a->tag, lane);
     }
-    if (lane == 0) {
-        s_svc_loaded = n_st;
-        s_dyn_b = a->dyn_from;
-    }
-}
-
-// Append piece p (one lane, holding s_svc_lock, s_svc_loaded == p, p >= dyn_from): the next
-// chunk of the dynamic tail, claimed from the current dynamic batch's device-scope counter;
-// past the last dynamic batch, the stop.  A claim that finds its batch exhausted moves the
-// block on to the next batch (every block leaves every dynamic batch through one such claim).
-__device__ __attribute__((noinline)) void svc_append_dyn(KArgs a, uint32_t p)
-{
-    SvcArea *area = &a->dev->area[a->launch & 1];
-    SvcSlot &s = s_svc[p % kSvcRing];
-    const SvcSlot &q = s_svc[(p + kSvcRing - 1) % kSvcRing];
-    const uint32_t stop_b = a->n_inline - 1;   // the inline stop
-    s.base = q.base + q.count;
-    s.done = 0;
-    s.dyn = 1;
-    for (;;) {
-        const uint32_t b = s_dyn_b;
-        if (b >= stop_b) {
-            s.stop = 1;
-            s.count = 0;
-            s.batch = stop_b;
-            break;
-        }
-        const SvcDescLite d = karg_desc(a, b);
-        const uint64_t T = (d.n + 63) / 64;
-        const uint64_t x = __hip_atomic_fetch_add(&area->ctr[b], (uint64_t)a->dyn_chunk, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if (x < T) {
-            s.stop = 0;
-            s.count = (uint32_t)(T - x < a->dyn_chunk ? T - x : a->dyn_chunk);
-            s.recs = d.recs;
-            s.bits = d.bits;
-            s.n = d.n;
-            s.stride = d.stride;
-            s.tile0 = x;
-            s.batch = b;
-            break;
-        }
-        s_dyn_b = b + 1;
-    }
-    __hip_atomic_store(&s_svc_loaded, p + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) s_svc_loaded = n_in;
 }
 
 // The wave has just entered batch b: if batch b + 1 is not loaded yet and nobody is loading,
@@ -1172,10 +1109,8 @@ __device__ __forceinline__ void svc_prefetch(KArgs a, uint32_t lane, uint32_t b)
         uint32_t expect = 0;
         if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1) {
-                if (b + 1 >= a->dyn_from) svc_append_dyn(a, b + 1);   // claim the next chunk ahead
-                else (void)svc_load(a, b + 1, false);
-            }
+            if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == b + 1)
+                (void)svc_load(a, b + 1, false);
             __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
@@ -1224,10 +1159,9 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
             if (__hip_atomic_compare_exchange_strong(&s_svc_lock, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_WORKGROUP)) {
                 r = 1;
-                if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == L) {
-                    if (L >= a->dyn_from) svc_append_dyn(a, L);
-                    else if (!svc_load(a, L, blocking)) r = 2;
-                }
+                if (__hip_atomic_load(&s_svc_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == L &&
+                    !svc_load(a, L, blocking))
+                    r = 2;
                 __hip_atomic_store(&s_svc_lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
@@ -1268,12 +1202,7 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
         s_svc_w = karg_cum(a, gridDim.x);
     }
     if (threadIdx.x < 64) svc_load_inline(a, lane);   // the batches posted before the launch
-    if (blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + 64) {   // the next grid's scratch
-        SvcArea *nx = &dev->area[(a->launch + 1) & 1];
-        nx->ctr[lane] = 0;
-        nx->bdone[lane] = 0;
-        if (lane == 0) nx->block_waits = 0;
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 64) dev->area[(a->launch + 1) & 1].block_waits = 0;   // next grid's
     // Block 0's last wave relays later-posted descriptors and forwards completions for the
     // grid's life.  It must not be alive at a barrier the other waves wait at (a wave still
     // running holds the barrier), so it passes the table-fill barrier without filling and
@@ -1340,14 +1269,11 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     uint32_t fl_b = 0, fl_count = 0, fl_k = 0;   // ... and the count they complete (fl_k = 0: none)
     uint32_t dc_b = 0, dc_count = 0, dc_k = 0;   // stored last iteration: count after this wait
     uint32_t pending = 0;            // verified tiles of cur.b not handed to a count yet
-    auto count = [&](uint32_t p, uint32_t cnt, uint32_t k) {   // stores acknowledged (caller waited)
+    auto count = [&](uint32_t b, uint32_t cnt, uint32_t k) {   // stores acknowledged (caller waited)
         if (k && lane == 0) {
-            SvcSlot &s = s_svc[p % kSvcRing];
-            const uint32_t old = __hip_atomic_fetch_add(&s.done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old + k == cnt) {   // the piece is verified
-                if (s.dyn) dyn_done(a, s.batch, cnt);
-                else svc_complete(dev, a->tag, s.batch);
-            }
+            const uint32_t old =
+                __hip_atomic_fetch_add(&s_svc[b % kSvcRing].done, k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old + k == cnt) svc_complete(dev, a->tag, b);
         }
     };
     auto store_stash = [&]() {

@@ -455,11 +455,10 @@ def test_service_live_submits_with_slow_host_link(ctx):
 
 
 @pytest.mark.parametrize("k", [3, 6, 9])
-def test_service_dynamic_tail_ragged(ctx, k):
-    """The dynamic tail of a run grid (the last 1-2 batches claimed in chunks from device-scope
-    counters, SvcArgs::dyn_from): ragged batch sizes (a partial last tile, chunks that end at a
-    batch's end), back-to-back grids (the per-grid scratch alternates), verdicts equal to the
-    launch path's for every batch; with HFV_SVC_DYN unset the tail is on at these sizes."""
+def test_service_run_ragged_large_batches(ctx, k):
+    """Run grids of large ragged batches (a partial last tile, block shares that end mid-tile),
+    back to back (the per-grid scratch alternates): verdicts equal to the launch path's for
+    every batch, no block waits for a descriptor, nothing relayed (all inline)."""
     ctx.key_add(0, orc.KEY_1111)
     base = 1 << 19
     sizes = [base + 37 * i + (i % 3) for i in range(k)]

@@ -182,7 +182,11 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
  * resident in LDS and verifies batches as the host posts them, with the same verdict
  * semantics as hfv_verify_records.  Batches are posted into a 256-entry descriptor ring in
  * pinned host memory; no kernel launch or table fill per batch, and a batch's tail
- * overlaps the next batch's start.
+ * overlaps the next batch's start.  Batches posted before the grid starts (hfv_service_run /
+ * run_async, submitv on a stopped service) travel in the launch's kernel arguments (up to 64),
+ * so those batches involve no PCIe round trip at all; batches posted to a running grid are
+ * fetched by one relay wave, up to 64 per host read, and their completions are forwarded to
+ * the ring by the same wave -- the verifying waves never access host memory.
  *   - Key-table, keysel or record-layout changes take effect at the next submit (the
  *     service is restarted there, after the batches already posted: a batch boundary).
  *   - Any other data-path call on the ctx (hfv_verify_records, hfv_br_process, ...) first
@@ -224,7 +228,8 @@ int hfv_service_run_async(hfv_ctx *ctx, const struct hfv_batch *batches, size_t 
  * exits): a ticket of a stopped grid reports done, or -EIO if that grid exited on its idle
  * timeout without verifying it. */
 /* 1 if the ticket's verdicts are complete in pass_bits (visible to any stream and to
- * copies), 0 if not yet. */
+ * copies), 0 if not yet.  A grid that has exited on the stop a run / run_async posted has
+ * verified every batch before it (its completions need not have been forwarded). */
 int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket);
 /* Wait until the ticket is complete; timeout_ms < 0 waits indefinitely.  -ETIMEDOUT on
  * timeout, -EIO if the service stopped before completing it. */

@@ -333,7 +333,10 @@ int hfv_br_set_hf_check(hfv_ctx *ctx, int enable);
  * the standard SCION path type (parser.h:140: VERDICT_NOT_IMPLEMENTED).  Default 0: all built.
  * -EINVAL (tables unchanged) if the installed tables hold an address of a switched-off family,
  * which br-loader rejects (maps.cpp:68-80 "Border router configuration contains IPv4 address,
- * but IPv4 support is deactivated."); hfv_br_set_config checks the same against the options. */
+ * but IPv4 support is deactivated."); hfv_br_set_config checks the same against the options.
+ * "Installed tables" are the ones last set by hfv_br_set_config or last loaded from an attached
+ * pinned config (hfv_ctx_attach_brconfig); a republished pinned config carries the options
+ * `hfv-loader attach` was given, and those replace the ones set here when it is reloaded. */
 #define HFV_BR_NO_IPV4 1u
 #define HFV_BR_NO_IPV6 2u
 #define HFV_BR_NO_SCION_PATH 4u

@@ -314,6 +314,7 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
                 return fail(-EINVAL, "attached router config holds counts past the fixed capacity; "
                                      "previous tables kept");
             const uint32_t off = ctx->br.hf_check_off;
+            ctx->cfg_src = cfg;   // what hfv_br_set_build_options checks against
             compile_br_config(&cfg, &ctx->br);
             ctx->br.hf_check_off = off;
             ctx->br.detached = detached;
@@ -325,11 +326,15 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         int next = ctx->active ^ 1;
         // wait (host) until the previous copy out of the staging image has been consumed
         HIP_TRY(hipEventSynchronize(ctx->img_free));
+        // the slot-major copy only for the service's gather variant (HFV_SVC_IFID=gather), the
+        // only reader: 64 KiB less per publish otherwise
+        static const bool gather = getenv("HFV_SVC_IFID") && !strcmp(getenv("HFV_SVC_IFID"), "gather");
         for (uint32_t k = 0; k < HFV_MAX_KEYS; ++k) {
             uint32_t dk[4 * kDevKeyRows];
             if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) compile_dev_key(&ctx->shadow[k], dk);
             else memset(dk, 0, sizeof dk);
             for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->keys.rows[r][k], dk + 4 * r, 16);
+            if (!gather) continue;
             uint32_t(*g)[4] = ctx->host_img->keys.gather[k];   // slot-major, rows 2..9 unrotated
             memcpy(g[0], dk, 16);
             memcpy(g[1], dk + 44, 16);
@@ -357,7 +362,14 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         ctx->nreaders[next] = 0;
         ctx->readers_overflow[next] = false;
         if (g_pub_delay_us) HIP_TRY((hipError_t)launch_debug_spin(st, g_pub_delay_us));
-        HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
+        if (gather) {
+            HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
+        } else {   // the key rows and valid bits, then the router tables (the gather rows stay unused)
+            HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, offsetof(DevKeyTable, gather),
+                                   hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(&ctx->dev_tab[next]->br, &ctx->host_img->br, sizeof(DevBrConfig),
+                                   hipMemcpyHostToDevice, st));
+        }
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
         ctx->dirty = false;

@@ -1045,7 +1045,9 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     // (a block's frames x the largest length); every launch adds into the same counters
     if (stats) {
         const uint64_t per_block = (uint64_t)(UINT32_MAX / (maxlen ? maxlen : 1));   // frames
-        uint64_t cap_n = (per_block > 64 ? per_block - 64 : 1) * (uint64_t)g.num_cus;   // + a tile of rounding
+        // a block's range is ceil(tiles / grid) tiles at most, i.e. up to a tile more than the even
+        // share plus a tile of rounding: reserve two tiles
+        uint64_t cap_n = (per_block > 128 ? per_block - 128 : 1) * (uint64_t)g.num_cus;
         if (g_br_split_override && g_br_split_override < cap_n) cap_n = g_br_split_override;
         if ((uint64_t)n > cap_n) {
             for (size_t off = 0; off < n; off += cap_n) {

@@ -206,31 +206,6 @@ __device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t
     }
 }
 
-// One tile in two halves (single key): the macinput, the whitening and rounds 1-2, then rounds
-// 3-10, the 48-bit compare and the ballot.  The resident service reads the next tile's claim
-// (an LDS atomic issued before the first half) between them, so the atomic's latency, queued
-// behind the CU's lookups, overlaps this tile's first rounds instead of stalling the wave.
-template <int TAB>
-__device__ __forceinline__ void tile_begin(const RecWords &r, const UniformKey &k, const Lane &l, uint32_t s[4])
-{
-    uint32_t w[4];
-    rec_macinput(r, w);
-    const uint4 k0 = k.row(0);
-    s[0] = w[0] ^ k0.x; s[1] = w[1] ^ k0.y; s[2] = w[2] ^ k0.z; s[3] = w[3] ^ k0.w;
-    round1_macinput<TAB>(s, k.row(11), l);
-    round_full<TAB>(s, k.template rk<TAB>(2), l);
-}
-template <int TAB>
-__device__ __forceinline__ uint64_t tile_finish(const RecWords &r, const UniformKey &k, const Lane &l, uint32_t s[4],
-                                                uint64_t t, uint64_t n, uint32_t lane)
-{
-#pragma unroll
-    for (int rr = 3; rr < 10; ++rr) round_full<TAB>(s, k.template rk<TAB>(rr), l);
-    uint32_t t0, t1;
-    round_last_48<TAB>(s, k.row(10), l, t0, t1);
-    return __ballot(t * 64 + lane < n && rec_tag_matches(r, t0, t1));
-}
-
 // Per-interface keys gathered into VGPRs (GatherKey) with the 4-table LDS layout: an internal
 // key-selection value for the kernels' template argument (the host still says
 // HFV_KEYSEL_IFID; the slot rule is the same, xdp.c:151-157).
@@ -831,11 +806,6 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 #ifndef HFV_SVC_AHEAD
 #define HFV_SVC_AHEAD 0
 #endif
-// HFV_SVC_SPLIT = 1 (default): single-key tiles in two halves around the read of the next
-// tile's claim (tile_begin / tile_finish); 0: the claim read at the top of the iteration.
-#ifndef HFV_SVC_SPLIT
-#define HFV_SVC_SPLIT 1
-#endif
 // Only wave 1 of every block samples (s_memtime from every wave of a CU slowed the loop
 // many times over); the other waves run the plain loop beside it.
 struct SvcProf {
@@ -1337,15 +1307,9 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
         GatherKey gk;
         if constexpr (KEYSEL == kKeyselGather) gk.issue(a->tab, rec_key_slot(rc));
         uint32_t g;
-        constexpr bool kSplit = HFV_SVC_SPLIT && KEYSEL == HFV_KEYSEL_ZERO && !HFV_SVC_AHEAD;
-        uint32_t sa[4];   // kSplit: the current tile's state after its first rounds
         if constexpr (HFV_SVC_AHEAD) {
             g = wave_uniform(gq);
             gq = claim();
-        } else if constexpr (kSplit) {
-            const uint32_t gc = claim();   // issued now, read after the tile's first rounds
-            if (keyok) tile_begin<TAB>(rc, ukey, l, sa);
-            g = wave_uniform(gc);
         } else {
             g = wave_uniform(claim());
         }
@@ -1360,12 +1324,8 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
         } else if constexpr (KEYSEL == kKeyselSched) {
             ballot = verify_tile_sched(rc, cur.tile, cur.n, lane, l);
         } else if (keyok) {
-            if constexpr (kSplit) {
-                ballot = tile_finish<TAB>(rc, ukey, l, sa, cur.tile, cur.n, lane);
-            } else {
-                RecWords c1[1] = {rc};
-                verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
-            }
+            RecWords c1[1] = {rc};
+            verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
         }
         if constexpr (HFV_SVC_PROF) prof.c[5] += 1;
         prof.mark(2);

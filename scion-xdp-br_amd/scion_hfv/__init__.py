@@ -598,6 +598,8 @@ class Ctx:
         waits of a block for a descriptor, descriptors in the kernel arguments."""
         v = (ctypes.c_uint64 * 8)()
         L = lib()
+        if not hasattr(L, "hfv_debug_service_relay"):   # an older build (A/B runs)
+            return None
         L.hfv_debug_service_relay.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         if L.hfv_debug_service_relay(self._h, v) != 0:
             return None

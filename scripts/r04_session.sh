@@ -33,3 +33,7 @@ if [[ $PART == 2 ]]; then
     step pmc_zero 400 bash scripts/pmc_round.sh zero svc rot8 || exit $?
     step pmc_ifid 400 bash scripts/pmc_round.sh ifid svc rot8 || exit $?
 fi
+if [[ $PART == br ]]; then   # where the router kernel's waves spend their cycles (diagnostic build)
+    # (build it first, in this container: scripts/mkvar_br.sh brprof -DHFV_BR_PROF=1)
+    HFV_LIB=$PWD/scion-xdp-br_amd/lib/ab/libscionhfv_brprof.so step br_phase 300 python scripts/br_phase_probe.py || exit $?
+fi

@@ -2084,6 +2084,20 @@ int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
     return rc;
 }
 
+// Diagnostic (not part of include/scion_hfv.h): the last grid's per-block stamps, s_memrealtime
+// (100 MHz): out[0 .. G) = after the table fill, out[G .. 2G) = the block's last completed share
+// (what svc_balance reads).  Returns G in *grid.
+int hfv_debug_service_blocks(hfv_ctx *ctx, uint64_t *out, size_t words, int *grid)
+{
+    if (!ctx || !out || !grid || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
+    const size_t g = ctx->svc_grid;
+    if (words < 2 * g) return fail(-EINVAL, "need %zu words", 2 * g);
+    *grid = (int)g;
+    int rc = svc_dev_read(ctx, out, offsetof(SvcDev, blk_start), g * 8);
+    if (!rc) rc = svc_dev_read(ctx, out + g, offsetof(SvcDev, blk_fin), g * 8);
+    return rc;
+}
+
 // Diagnostic (not part of include/scion_hfv.h): the last grid's relay counters (SvcRelayStat,
 // 8 words): the host round trip probed at grid start, host reads and their summed / longest
 // round trips (100 MHz ticks), descriptors relayed, completions forwarded, waits of a block for

@@ -730,7 +730,7 @@ __device__ __forceinline__ uint64_t karg_cum(KArgs a, uint64_t k)
     return svc_cum(w, k);
 }
 
-struct SvcSlot {
+struct alignas(16) SvcSlot {
     uint32_t base, count;   // block tile numbers [base, base + count)
     uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
     uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the block's range
@@ -768,9 +768,9 @@ __device__ __forceinline__ RecWords load_tile(const SvcTile &t, uint32_t lane, u
     const GlobalU8 *p = (const GlobalU8 *)(t.recs + first * t.stride) + off;
     typedef const __attribute__((address_space(1))) u32x2 *P2;
     typedef const __attribute__((address_space(1))) uint32_t *P1;
+    RecWords r;
     const u32x2 a = *reinterpret_cast<P2>(p + inf_off);
     const u32x2 b = *reinterpret_cast<P2>(p + hf_off);
-    RecWords r;
     r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
@@ -1130,16 +1130,24 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
     for (;;) {
         const uint32_t L =
             wave_uniform(__hip_atomic_load(&s_svc_loaded, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-        uint32_t lo = L > kSvcRing ? L - kSvcRing : 0u;
+        // The slots hold batches [L - kSvcRing, L); the oldest one's slot is the one a loader
+        // of batch L overwrites, possibly right now, and that batch is verified (the host posts
+        // ticket t only after ticket t - kSvcRing completed), so g never lies in it: skip it.
+        uint32_t lo = L >= kSvcRing ? L - kSvcRing + 1 : 0u;
         if (mb > lo) lo = mb;
-        // newest loaded batch starting at or before g
-        for (uint32_t b = L; b-- > lo;) {
+        // the loaded batch holding g, searched forward from the wave's current batch (g only
+        // grows, so it is almost always mb or mb + 1; a backward search from the newest
+        // loaded batch cost one dependent LDS round trip per batch posted ahead: ~10 per
+        // batch change when a run's 20 batches are all inline).  Slot header {base, count,
+        // done, stop} in one 16-byte read.
+        for (uint32_t b = lo; b < L; ++b) {
             const SvcSlot &s = s_svc[b % kSvcRing];
-            const uint32_t base = wave_uniform(s.base);
-            if ((int32_t)(g - base) < 0) continue;
-            if (wave_uniform(s.stop)) return kSvcStop;
-            const uint32_t count = wave_uniform(s.count);
-            if (g - base >= count) break;   // g is beyond the loaded batches
+            const uint4 h = *reinterpret_cast<const uint4 *>(&s);
+            const uint32_t base = wave_uniform(h.x);
+            if ((int32_t)(g - base) < 0) break;   // before this batch: not loaded (cannot happen)
+            if (wave_uniform(h.w)) return kSvcStop;
+            const uint32_t count = wave_uniform(h.y);
+            if (g - base >= count) continue;      // in a later batch
             t.recs = wave_uniform64(s.recs);
             t.bits = wave_uniform64(s.bits);
             t.n = wave_uniform64(s.n);

@@ -1992,14 +1992,19 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
         if (lr) return lr;
     }
     clock_gettime(CLOCK_MONOTONIC, &t_launch);
-    if (!wait) return rc;   // the grid exits after the stop posted behind the batches
+    static const bool trace = getenv("HFV_SVC_TRACE") != nullptr;   // diagnostics
+    auto us = [](const timespec &a, const timespec &b) {
+        return (b.tv_sec - a.tv_sec) * 1e6 + (b.tv_nsec - a.tv_nsec) / 1e3;
+    };
+    if (!wait) {   // the grid exits after the stop posted behind the batches
+        if (trace)
+            fprintf(stderr, "hfv_service_run_async: checks+guard+quiesce %.1f us, begin %.1f us, posts %.1f us, "
+                    "launch call %.1f us\n", us(t_in, t_chk), us(t_chk, t_beg), us(t_beg, t_post), us(t_post, t_launch));
+        return rc;
+    }
     int sr = svc_stop(ctx, kernel_ms);
     clock_gettime(CLOCK_MONOTONIC, &t_done);
-    static const bool trace = getenv("HFV_SVC_TRACE") != nullptr;   // diagnostics
     if (trace) {
-        auto us = [](const timespec &a, const timespec &b) {
-            return (b.tv_sec - a.tv_sec) * 1e6 + (b.tv_nsec - a.tv_nsec) / 1e3;
-        };
         fprintf(stderr,
                 "hfv_service_run: checks+guard+quiesce %.1f us, begin %.1f us, posts %.1f us, launch call %.1f us, "
                 "launch return -> grid exit seen %.1f us, grid %.1f us\n",

@@ -7,7 +7,7 @@
 # time-out stops the script (nothing else touches the GPU afterwards).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r04_final
+OUT=gpurun_out/${R04_OUT:-r04_final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() {   # step <name> <timeout-s> <cmd...>

@@ -67,10 +67,16 @@ def blocks():
     assert L.hfv_debug_service_blocks(ctx._h, blk, 4096, ctypes.byref(g)) == 0
     a = np.array(blk[:2 * g.value], dtype=np.int64)
     st, fin = a[:g.value], a[g.value:]
+    f = (fin - st.min()) / 100.0
+    detail.append({"block0": round(float(f[0] - np.median(f)), 2),
+                   "xcd_median": [round(float(np.median(f[x::8]) - np.median(f)), 2) for x in range(8)],
+                   "slowest": [(int(k), round(float(f[k] - np.median(f)), 2)) for k in np.argsort(f)[-6:]],
+                   "fastest": [(int(k), round(float(f[k] - np.median(f)), 2)) for k in np.argsort(f)[:3]]})
     return (np.median(fin) - st.min()) / 100.0, (fin.max() - fin.min()) / 100.0, (st.max() - st.min()) / 100.0
 
 
 spans = {16: [], 4: [], 1: []}
+detail = []
 rows = {"launch": [], 16: [], 4: [], 1: []}
 for rep in range(REPS + 1):
     ms = ctx.verify_records_timed(big, N, bits, stream=sh)
@@ -94,4 +100,6 @@ for k, r in spans.items():
     a = np.array(r)
     print(f"{k:>6}: block finish median {np.median(a[:, 0]):7.1f} us after the first fill, finish spread "
           f"{np.median(a[:, 1]):6.1f} us, fill spread {np.median(a[:, 2]):5.1f} us", flush=True)
+for d in detail[-6:]:
+    print(d)
 ctx.close()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B of library builds on the bench headline (one bench.py process per run,
-HFV_LIB selecting the build):  python scripts/ab_libs.py ROUNDS lib1.so lib2.so[@VAR=VAL,...] ... [-- bench args]
-(a spec's @VAR=VAL,... sets environment variables for that run: the same build with a switch)
+HFV_LIB selecting the build):  python scripts/ab_libs.py ROUNDS lib1.so lib2.so[@VAR=VAL|...] ... [-- bench args]
+(a spec's @VAR=VAL|VAR2=VAL2 sets environment variables for that run: the same build with a switch;
+values may contain commas, e.g. lib.so@HFV_KVARIANT=block=512,bpc=2,tab=2)
 Prints one line per run: build, value (Mpkt/s), grid ms, shader MHz, launch-path Mpkt/s."""
 import json
 import os
@@ -24,7 +25,7 @@ def main():
         for spec in libs:
             lib, _, envs = spec.partition("@")
             env = dict(os.environ, HFV_LIB=os.path.abspath(lib))
-            env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
+            env.update(kv.split("=", 1) for kv in envs.split("|") if kv)
             p = subprocess.run(bench, capture_output=True, text=True, env=env, timeout=240)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
             if p.returncode != 0 or not line:

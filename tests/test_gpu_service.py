@@ -484,3 +484,56 @@ def test_service_run_ragged_large_batches(ctx, k):
             assert torch.equal(o, w), f"batch {i}"
     rel = ctx.service_relay()
     assert rel["block_waits"] == 0 and rel["relayed"] == 0, rel
+
+
+@pytest.mark.parametrize("keysel", [0, 1])
+def test_service_soak_random_shapes(ctx, keysel):
+    """A short soak (scripts/svc_soak.py runs the long form): grids of random shape -- K from 1
+    to 300 (inline, relayed, past the ring), batch sizes from 1 to 2^18 records at random
+    64-aligned offsets, through hfv_service_run, run_async and live submits in bursts -- for a
+    few seconds; every bitmap must equal the launch path's over the same records."""
+    import random
+    rng = random.Random(11 + keysel)
+    n_all = 1 << 19
+    recs = torch.empty((n_all, 64), dtype=torch.uint8, device=DEV)
+    if keysel:
+        ctx.key_add_batch(0, bytes(rng.randrange(256) for _ in range(256 * 16)))   # 256 interface keys
+        ctx.set_keysel(hfv.KEYSEL_IFID)
+    else:
+        ctx.key_add(0, orc.KEY_1111)
+    ctx.gen_records(recs, n_all, 0x5C100001, first_index=0)
+    ref = new_bits(n_all)
+    ctx.verify_records(recs, n_all, ref)
+    ref_bits = np.unpackbits(bits_np(ref, n_all).view(np.uint8), bitorder="little")
+    grids = 0
+    t_end = time.time() + 4.0
+    while time.time() < t_end:
+        k = rng.choice([1, 2, 20, 64, 65, 300])
+        shape = []
+        for _ in range(k):
+            n = rng.choice([1, 63, 64, 65, 1000, 65536, 1 << 18])
+            shape.append(((rng.randrange(0, n_all - n + 1) & ~63), n))
+        outs = [new_bits(n, fill=-1) for _, n in shape]
+        specs = [(recs[off:off + n], n, o) for (off, n), o in zip(shape, outs)]
+        torch.cuda.synchronize()
+        mode = rng.choice(["run", "async", "live"])
+        if mode == "run":
+            ctx.service_run(specs)
+        elif mode == "async":
+            ctx.service_run_async(specs)
+            torch.cuda.synchronize()
+            ctx.service_stop()
+        else:
+            ts = []
+            for i in range(0, len(specs), 7):
+                ts += ctx.service_submitv(specs[i:i + 7])
+            for t in ts:
+                ctx.service_wait(t, 20000)
+            ctx.service_stop()
+        for (off, n), o in zip(shape, outs):
+            want = np.zeros(((n + 63) // 64) * 64, dtype=np.uint8)
+            want[:n] = ref_bits[off:off + n]
+            assert np.array_equal(bits_np(o, n), np.packbits(want, bitorder="little").view(np.uint64)), \
+                (grids, mode, k, off, n)
+        grids += 1
+    assert grids >= 10

@@ -2089,9 +2089,10 @@ int hfv_debug_service_clocks(hfv_ctx *ctx, uint64_t *out)
     return rc;
 }
 
-// Diagnostic (not part of include/scion_hfv.h): the last grid's per-block stamps, s_memrealtime
-// (100 MHz): out[0 .. G) = after the table fill, out[G .. 2G) = the block's last completed share
-// (what svc_balance reads).  Returns G in *grid.
+// Diagnostic (not part of include/scion_hfv.h): the last grid's per-block stamps: out[0 .. G)
+// = s_memrealtime (100 MHz) after the table fill, out[G .. 2G) = at the block's last completed
+// share (what svc_balance reads); with words >= 4G also s_memtime (the shader clock) at those two
+// points in out[2G .. 3G) and out[3G .. 4G).  Returns G in *grid.
 int hfv_debug_service_blocks(hfv_ctx *ctx, uint64_t *out, size_t words, int *grid)
 {
     if (!ctx || !out || !grid || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
@@ -2100,6 +2101,8 @@ int hfv_debug_service_blocks(hfv_ctx *ctx, uint64_t *out, size_t words, int *gri
     *grid = (int)g;
     int rc = svc_dev_read(ctx, out, offsetof(SvcDev, blk_start), g * 8);
     if (!rc) rc = svc_dev_read(ctx, out + g, offsetof(SvcDev, blk_fin), g * 8);
+    if (!rc && words >= 4 * g) rc = svc_dev_read(ctx, out + 2 * g, offsetof(SvcDev, blk_clk0), g * 8);
+    if (!rc && words >= 4 * g) rc = svc_dev_read(ctx, out + 3 * g, offsetof(SvcDev, blk_clk1), g * 8);
     return rc;
 }
 

@@ -155,6 +155,9 @@ struct SvcDev {   // device memory: written by the grid; the host copies what it
     // last completed its share of a batch
     uint64_t blk_start[kSvcMaxBlocks];
     uint64_t blk_fin[kSvcMaxBlocks];
+    // s_memtime (shader clock) at the same two points: each block's clock over its loop
+    uint64_t blk_clk0[kSvcMaxBlocks];
+    uint64_t blk_clk1[kSvcMaxBlocks];
     // HFV_SVC_SPAN builds: s_memrealtime at each block's entry and after its table fill, and at
     // each wave's exit (block * 16 + wave)
     uint64_t span_entry[kSvcMaxBlocks];

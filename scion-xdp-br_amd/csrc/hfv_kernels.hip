@@ -850,6 +850,7 @@ struct SvcProf {
 __device__ __attribute__((noinline)) void svc_complete(SvcDev *dev, uint64_t tag, uint32_t b)
 {
     dev->blk_fin[blockIdx.x] = __builtin_amdgcn_s_memrealtime();   // read by the host after the grid
+    dev->blk_clk1[blockIdx.x] = __builtin_amdgcn_s_memtime();
     __hip_atomic_store(&dev->done[b % kSvcRing][blockIdx.x], tag | ((uint64_t)b + 1), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1231,7 +1232,10 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
         if (!relay) fill_keys3(a->tab, nthr);
     }
     __syncthreads();
-    if (threadIdx.x == 0) dev->blk_start[blockIdx.x] = memrealtime();
+    if (threadIdx.x == 0) {
+        dev->blk_start[blockIdx.x] = memrealtime();
+        dev->blk_clk0[blockIdx.x] = __builtin_amdgcn_s_memtime();
+    }
     if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_fill[blockIdx.x] = memrealtime();
     if (relay) {   // no barrier follows: the block's other waves go on without it
         svc_relay(a, lane, gridDim.x);

@@ -54,7 +54,10 @@ def launch_mhz():
     check()
     st = stamps.cpu().numpy()[: grid.value * 16]
     st = st[st[:, 0] != 0]
-    return float(np.median((st[:, 13] - st[:, 12]) / np.maximum(1, st[:, 15] - st[:, 1]) * 100.0))
+    m = (st[:, 13] - st[:, 12]) / np.maximum(1, st[:, 15] - st[:, 1]) * 100.0
+    xcc = (st[:, 14].astype(np.uint64) >> np.uint64(32)) & np.uint64(0xf)
+    launch_xcd.append([round(float(np.median(m[xcc == x])), 0) if (xcc == x).any() else None for x in range(8)])
+    return float(np.median(m))
 
 
 blk = (ctypes.c_uint64 * 4096)()
@@ -65,10 +68,13 @@ def blocks():
     """last grid: (median block finish - first fill, max - min finish) in us"""
     g = ctypes.c_int()
     assert L.hfv_debug_service_blocks(ctx._h, blk, 4096, ctypes.byref(g)) == 0
-    a = np.array(blk[:2 * g.value], dtype=np.int64)
-    st, fin = a[:g.value], a[g.value:]
+    G = g.value
+    a = np.array(blk[:4 * G], dtype=np.int64)
+    st, fin, c0, c1 = a[:G], a[G:2 * G], a[2 * G:3 * G], a[3 * G:]
+    mhz = (c1 - c0) / np.maximum(1, fin - st) * 100.0
     f = (fin - st.min()) / 100.0
     detail.append({"block0": round(float(f[0] - np.median(f)), 2),
+                   "xcd_mhz": [round(float(np.median(mhz[x::8])), 0) for x in range(8)],
                    "xcd_median": [round(float(np.median(f[x::8]) - np.median(f)), 2) for x in range(8)],
                    "slowest": [(int(k), round(float(f[k] - np.median(f)), 2)) for k in np.argsort(f)[-6:]],
                    "fastest": [(int(k), round(float(f[k] - np.median(f)), 2)) for k in np.argsort(f)[:3]]})
@@ -77,6 +83,7 @@ def blocks():
 
 spans = {16: [], 4: [], 1: []}
 detail = []
+launch_xcd = []
 rows = {"launch": [], 16: [], 4: [], 1: []}
 for rep in range(REPS + 1):
     ms = ctx.verify_records_timed(big, N, bits, stream=sh)
@@ -102,4 +109,6 @@ for k, r in spans.items():
           f"{np.median(a[:, 1]):6.1f} us, fill spread {np.median(a[:, 2]):5.1f} us", flush=True)
 for d in detail[-6:]:
     print(d)
+for x in launch_xcd[-3:]:
+    print("launch xcd_mhz", x)
 ctx.close()

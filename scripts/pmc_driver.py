@@ -2,7 +2,8 @@
 """Workload for rocprofv3 --pmc passes: verify 2^20 and 2^24 records (config 2, and config 3
 with --keysel ifid), `reps` launches each, after one untimed generation pass.  With a 4th
 argument `svc` the batches go through the resident service instead: per size one 2-batch
-grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches.  With a 5th
+grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches (`svcrun`: the
+same grids through hfv_service_run, every batch in the kernel arguments).  With a 5th
 argument `rotR` each size is held in R resident batches and batch k of a grid verifies
 batch k % R, exactly as bench.py's headline does (R x 64 MiB > the Infinity Cache)."""
 import os
@@ -46,7 +47,8 @@ def main():
         return run_br(int(sys.argv[2]) if len(sys.argv) > 2 else 10)
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
-    svc = len(sys.argv) > 4 and sys.argv[4] == "svc"
+    svc = len(sys.argv) > 4 and sys.argv[4] in ("svc", "svcrun")
+    run = len(sys.argv) > 4 and sys.argv[4] == "svcrun"   # the batches inline (hfv_service_run)
     rot = int(sys.argv[5][3:]) if len(sys.argv) > 5 and sys.argv[5].startswith("rot") else 1
     torch.cuda.set_device(0)
     ctx = hfv.Ctx(0)
@@ -58,12 +60,15 @@ def main():
     for n in sizes:
         R = rot if n <= (1 << 20) else 1
         recs = [torch.empty((n, 64), dtype=torch.uint8, device="cuda") for _ in range(R)]
-        bits = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(max(R, reps))]
+        bits = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(max(R, reps, 2))]
         for i, r in enumerate(recs):   # consecutive generator dispatches = one size group (pmc_summary.py)
             ctx.gen_records(r, n, SEED_RECORDS, first_index=i * n)
         if svc:
             torch.cuda.synchronize()
             for k in (2, reps):
+                if run:
+                    ctx.service_run([(recs[j % R], n, bits[j]) for j in range(k)])
+                    continue
                 ctx.service_start()
                 ctx.service_submitv([(recs[j % R], n, bits[j]) for j in range(k)])
                 ctx.service_stop()

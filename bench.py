@@ -118,6 +118,15 @@ def popcount(bits_t):
     return int(np.unpackbits(b).sum())
 
 
+def truth_bitmap(n, first_index):
+    """The exact verdict bitmap of generated records [first_index, first_index + n): record i
+    passes iff its MAC was not corrupted (DESIGN.md section 3), bit i % 64 of word i // 64."""
+    ok = ~corrupted(n, first_index)
+    padded = np.zeros(((n + 63) // 64) * 64, dtype=bool)
+    padded[:n] = ok
+    return np.packbits(padded.reshape(-1, 8), axis=1, bitorder="little").reshape(-1).view(np.int64)
+
+
 # ---- launcher --------------------------------------------------------------------------------
 
 def free_port():
@@ -339,11 +348,14 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         ctx.gen_records(b, n, SEED_RECORDS, first_index=first + i * n, stream=stream)
     nb = max(R, min(steps, bitmap_cap))
     bitmaps = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(nb)]
-    expect = [expected_pass_count(n, first + i * n) for i in range(R)]
+    # the exact verdict bitmap of every resident batch (generator truth), on the device
+    truth = [torch.from_numpy(truth_bitmap(n, first + i * n)).cuda() for i in range(R)]
 
     def check(k_steps):
+        """Every bitmap the last k_steps steps wrote equals its batch's truth bit for bit (untimed)."""
+        torch.cuda.synchronize()
         for k in range(min(k_steps, nb)):
-            assert popcount(bitmaps[k]) == expect[k % R], f"bitmap {k} disagrees with generator truth"
+            assert torch.equal(bitmaps[k], truth[k % R]), f"bitmap {k} != the generator truth of batch {k % R}"
 
     # --- launch path: one hfv_verify_records launch (+ table fill) per batch ---
     for k in range(max(warmup, R)):                 # >= one untimed pass over every batch
@@ -445,6 +457,68 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
                                "relayed": r[6]["relayed"], "block_waits": r[6]["block_waits"]}
                               for r in list(runs if not timed_value else []) + truns if r[6]],
                 "svc_value_regions": "timed with dispatch events" if timed_value else "no timing events"})
+    return out
+
+
+SUSTAINED_STEPS = 200   # batches in the sustained leg's grid (~2.3 ms: the power-limited clock)
+FEED_DEPTH = 4          # batches in flight in INTEGRATION.md section 2's feeder loop
+
+
+def service_legs(hfv, W, ctx, m, n, first, rotate, steps):
+    """Two more views of the headline's service on the same resident batches (every rank, after
+    the headline regions; untimed setup, bitmaps checked bit-exactly against generator truth):
+      sustained -- one grid over SUSTAINED_STEPS batches: long enough for the chip to settle at
+                   the clock its power limit allows under this load (the K = 20 headline grid is a
+                   0.22 ms burst at ~2.0 GHz; the XDP program it replaces runs continuously);
+      per_call  -- the data-plane binding INTEGRATION.md section 2 documents, run in C through
+                   hfv_debug_feed_loop on a resident grid: per RX batch one hfv_service_submit, and
+                   hfv_service_wait on the ticket FEED_DEPTH batches back; host clock, steady state
+                   (the grid was started and warmed before the clock)."""
+    torch = W.torch
+    batches, R = m["batches"], rotate
+    truth = [torch.from_numpy(truth_bitmap(n, first + i * n)).cuda() for i in range(R)]
+    out = {}
+    # sustained
+    K = SUSTAINED_STEPS
+    bms = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(K)]
+    posts = ctx.service_batches([(batches[k % R], n, bms[k]) for k in range(K)])
+    W.sync()
+    W.barrier()
+    ctx.service_set_timing(True)
+    _, g_ms = ctx.service_run(posts)
+    mhz = ctx.service_shader_mhz()
+    W.sync()
+    for k in range(K):
+        assert torch.equal(bms[k], truth[k % R]), f"sustained: bitmap {k} != generator truth"
+    g_all = W.gather(g_ms)
+    ach = BYTES_PER_PACKET * n * K / (max(g_all) * 1e-3) / 1e9
+    out["sustained"] = {"batches": K, "grid_ms": round(g_ms, 4), "mpkts": round(W.size * n * K / max(g_all) / 1e3, 1),
+                        "frac": round(ach / HBM_PEAK_GBS / W.size, 4), "shader_mhz": round(mhz, 1) if mhz else None,
+                        "per_rank_grid_ms": [round(x, 4) for x in g_all],
+                        "note": f"one service grid over {K} resident batches (k % {R}): the clock the power limit "
+                                f"holds under continuous verify; frac per GPU"}
+    del bms
+    # per_call: the documented feeder loop on a running grid
+    bms = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(steps)]
+    warm = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+    posts = ctx.service_batches([(batches[k % R], n, bms[k]) for k in range(steps)])
+    W.sync()
+    W.barrier()   # before the grid starts: no collective may need the CUs a resident grid holds
+    ctx.service_start()
+    ctx.feed_loop(ctx.service_batches([(batches[0], n, warm)]), depth=1)   # grid up, tables filled
+    el = ctx.feed_loop(posts, depth=FEED_DEPTH)
+    ctx.service_stop()
+    W.sync()
+    for k in range(steps):
+        assert torch.equal(bms[k], truth[k % R]), f"per_call: bitmap {k} != generator truth"
+    el_all = W.gather(el)
+    out["per_call"] = {"mpkts": round(W.size * n * steps / max(el_all) / 1e6, 1),
+                       "frac": round(BYTES_PER_PACKET * n * steps / max(el_all) / 1e9 / HBM_PEAK_GBS, 4),
+                       "us_per_batch": round(max(el_all) / steps * 1e6, 2), "batches": steps, "depth": FEED_DEPTH,
+                       "path": "INTEGRATION.md section 2: hfv_service_submit per batch + hfv_service_wait on the "
+                               f"ticket {FEED_DEPTH} back, in C (hfv_debug_feed_loop), on a resident grid; host clock; "
+                               "frac per GPU"}
+    del bms
     return out
 
 
@@ -866,10 +940,12 @@ def run_hf(args, W):
     stream = torch.cuda.current_stream().cuda_stream
     cus = torch.cuda.get_device_properties(W.device).multi_processor_count
     tb = apply_thread_budget(args, thread_budget(W, ctx))
+    svc_blocks = 0
     if args.same_device and W.size > 1:
         # ranks sharing one GPU: each service grid takes its share of the CUs (one block per CU
         # holds the CU's LDS), so the grids run side by side instead of one after the other
-        os.environ["HFV_SVC_GRID"] = str(max(1, cus // W.size))
+        svc_blocks = max(1, cus // W.size)
+        ctx.service_set_grid(svc_blocks)
     m = measure_hf(hfv, W, ctx, args.keysel, n, first, args.rotate, args.steps, args.warmup, stream, reps=args.svc_reps,
                    service=not args.launch_only)
     # every rank's median event-timed grid (the service's kernel time per rank), and no rank starts
@@ -947,9 +1023,13 @@ def run_hf(args, W):
     }
     if args.same_device:
         result["same_device"] = {"ranks": W.size, "physical_gpus": 1,
-                                 "service_grid_blocks": os.environ.get("HFV_SVC_GRID"),
+                                 "service_grid_blocks": svc_blocks,
                                  "note": "launcher rehearsal: every rank on GPU 0"}
     recs0, bits0 = m["batches"][0], m["bitmaps"][0]
+    ref_bits = bits0.cpu().numpy().view(np.uint64).copy()   # the headline's own bitmap of batch 0
+    if not args.no_extras and not args.launch_only:
+        settle(args)
+        result.update(service_legs(hfv, W, ctx, m, n, first, args.rotate, args.steps))
     extras = W.size == 1 and not args.no_extras
 
     if extras:   # the same batch re-posted: served from the Infinity Cache (diagnostic)
@@ -995,7 +1075,6 @@ def run_hf(args, W):
                                   "service_shader_mhz": round(smhz, 1) if smhz else None}
         del big, bbits
 
-    ref_bits = bits0.cpu().numpy().view(np.uint64).copy()
     if extras and keysel == hfv.KEYSEL_ZERO:   # config 3 beside the config-2 headline
         settle(args)
         ctx3 = make_ctx(hfv, W.device, hfv.KEYSEL_IFID)
@@ -1043,8 +1122,13 @@ def run_hf(args, W):
 
     if extras:
         result["settle_s_before_extra_legs"] = args.settle_s
-    if W.rank == 0 and W.size == 1 and args.cpu_budget > 0:
+    # every rank's GPU work is done before the CPU baseline runs (it shares the host with them)
+    W.barrier()
+    if W.rank == 0 and args.cpu_budget > 0:
         result["cpu_baseline"] = cpu_baseline(recs0.cpu().numpy(), keysel, ref_bits, args.cpu_budget)
+        if W.size > 1:
+            result["cpu_baseline"]["note"] = (f"rank 0 after all {W.size} ranks finished their GPU legs, its "
+                                              f"threads on GPU 0's share of the host")
 
     if W.rank == 0:
         print(json.dumps(result), flush=True)

@@ -243,6 +243,11 @@ int hfv_service_running(const hfv_ctx *ctx);
  * The events cost the runtime ~12 us per launch-to-synchronize round trip on MI355X (7.5 us of
  * host time in the launch call, profiles/r03/launch_cost/), which a short run can leave out. */
 int hfv_service_set_timing(hfv_ctx *ctx, int enable);
+/* Service grids started from now on use `blocks` blocks (one per CU at most; 0 = one per CU,
+ * the default).  For several processes sharing one GPU, each with its own service: every grid
+ * holds the LDS of the CUs it runs on, so grids of cus/ranks blocks run side by side.  Stops
+ * a running grid after its posted batches. */
+int hfv_service_set_grid(hfv_ctx *ctx, int blocks);
 
 /* ---- key-schedule kernels ------------------------------------------------------------
  * AES-128 key expansion + CMAC K1 on the GPU, one key per lane: device raw keys[n] ->

@@ -59,6 +59,12 @@ __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_
 // slower in the kernel (2^24 records: 257.5 vs 235.5 us, profiles/r01/addr_bitop3.log): the
 // verify loop is bound by LDS issue and the lookup chain's latency, not by VALU throughput,
 // and the second dependent instruction lengthens the address -> ds_read chain.
+// HFV_B1_BITOP3 = 1 (A/B builds only): byte-1 lookups addressed by the full-rate v_bitop3
+// form instead of v_perm (round 2: 8 % fewer VALU cycles, neutral at the ~2.0 GHz of a short
+// grid; VERDICT r04 #5 asks for it at the power-limited clock of a sustained one).
+#ifndef HFV_B1_BITOP3
+#define HFV_B1_BITOP3 0
+#endif
 struct Lane;
 template <int TAB, int K>
 __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l);
@@ -83,84 +89,6 @@ __device__ __forceinline__ void fill_ttab()
         dst[e] = rot ? __builtin_amdgcn_alignbit(t, t, 32 - rot) : t;
     }
 }
-
-// Same tables copied into LDS by LDS-DMA: one global_load_lds_dwordx4 writes 1 KiB of LDS per
-// wave-instruction, no VGPR round trip and ~16x fewer instructions than fill_ttab.  The source
-// is the compact image (k_build_ttab_image): the 64 lanes of LDS chunk c (8 runs of 32 lane
-// copies) read entries 8c .. 8c + 7, 8 lanes per 16-byte entry, so a block reads 16 KiB from L2
-// instead of the 128 KiB it writes (round 3 copied a 128 KiB replicated image: 4.4-5 us from
-// block entry to the fill barrier, the whole chip pulling 32 MiB through L2 at every grid start).
-__device__ __forceinline__ const char *ttab_src(const uint32_t *img, uint32_t chunk, uint32_t lane)
-{
-    return reinterpret_cast<const char *>(img) + (size_t)((chunk << 3) + (lane >> 3)) * 16;
-}
-
-// Issue-only form with the block size known at compile time (reading blockDim would add a
-// dispatch-packet load whose wait also drains the record loads issued before the fill).
-template <int TAB, int BLOCK>
-__device__ __forceinline__ void fill_ttab_dma_issue(const uint32_t *__restrict__ img)
-{
-    constexpr int kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
-    constexpr int nw = BLOCK / 64;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-    for (int c = wave; c < kChunks; c += nw) {
-        const char *src = ttab_src(img, c, lane);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
-    }
-}
-
-// Issue-only form for `nw` filling waves (wave index `wave` < nw) of a block some of whose
-// waves do other work.
-template <int TAB>
-__device__ __forceinline__ void fill_ttab_dma_issue_n(const uint32_t *__restrict__ img, uint32_t wave, uint32_t nw)
-{
-    constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
-    const int lane = threadIdx.x & 63;
-    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-    for (uint32_t c = wave; c < kChunks; c += nw) {
-        const char *src = ttab_src(img, c, lane);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
-    }
-}
-
-// The same copy through VGPRs: each filling wave loads its chunks' 16-byte pieces from the
-// compact image (global_load_dwordx4, all issued at once), then writes them with
-// ds_write_b128 (≈79 B/clk/CU).  issue() and commit() are split so a kernel can put other
-// loads (a first tile's records) between them: vmcnt retires in order, so the table pieces,
-// issued first, can be written while those are still in flight.  For 15 or 16 filling waves.
-template <int TAB>
-struct TtabRegs {
-    static constexpr uint32_t kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
-    static constexpr int kMax = (int)((kChunks + 14) / 15);
-    uint4 v[kMax];
-    __device__ __forceinline__ void issue(const uint32_t *__restrict__ img, uint32_t wave, uint32_t nw)
-    {
-        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-        const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-        for (int k = 0; k < kMax; ++k) {
-            const uint32_t c = wave + k * nw;
-            if (c < kChunks) {
-                typedef const __attribute__((address_space(1))) v4 *G4;
-                const v4 x = *(G4)(ttab_src(img, c, lane));   // global, not flat: vmcnt only
-                v[k] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-        }
-    }
-    __device__ __forceinline__ void commit(uint32_t wave, uint32_t nw) const
-    {
-        const uint32_t lane = threadIdx.x & 63;
-        char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-#pragma unroll
-        for (int k = 0; k < kMax; ++k) {
-            const uint32_t c = wave + k * nw;
-            if (c < kChunks) *reinterpret_cast<uint4 *>(lds + c * 1024 + lane * 16) = v[k];
-        }
-    }
-};
 
 // The tables written from T0 in the kernel arguments (constant address space, one memory hop
 // with the rest of the arguments): every filling lane loads T0 of its chunks' runs and writes
@@ -191,23 +119,6 @@ __device__ __forceinline__ void fill_ttab_karg(P t0, uint32_t wave, uint32_t nw)
     }
 }
 
-template <int TAB>
-__device__ __forceinline__ void fill_ttab_dma(const uint32_t *__restrict__ img)
-{
-    constexpr int kChunks = (TAB == 4 ? 131072 : 65536) / 1024;
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    char *lds = TAB == 4 ? reinterpret_cast<char *>(s_tab128) : reinterpret_cast<char *>(s_tab64);
-    for (int c = wave; c < kChunks; c += nw) {
-        const char *src = ttab_src(img, c, lane);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)(lds + c * 1024), 16, 0, 0);
-    }
-    // vmcnt retires in issue order; the DMA pieces are the youngest loads, and the record
-    // loads issued before them must complete as well before the barrier (the compiler
-    // inserts that wait anyway), so a full drain is the correct and only wait here.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // nthr: the block's threads 0..nthr-1 share the copy (0: all of them)
 __device__ __forceinline__ void fill_keys(const DevKeyTable *tab, uint32_t nthr = 0)
 {
@@ -234,7 +145,11 @@ __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l
         const uint32_t a3 = (__builtin_amdgcn_ubfe(w, 8 * K, 8) << (kTab3Log + 2)) | base;
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab32) + a3);
     }
-    const uint32_t a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
+    uint32_t a;
+    if constexpr (HFV_B1_BITOP3 && K == 1)   // (w & 0xff00) | base: one full-rate v_bitop3_b32
+        a = __builtin_amdgcn_bitop3_b32(w, 0xff00u, base, 0xEA);
+    else
+        a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
     const char *t = TAB == 4 ? reinterpret_cast<const char *>(s_tab128) : reinterpret_cast<const char *>(s_tab64);
     return *reinterpret_cast<const uint32_t *>(t + a);
 }
@@ -381,100 +296,64 @@ struct LdsKey {              // per-lane slot from the LDS copy of the table
     __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
 };
 
-// Per-lane slot with the packet's key rows gathered from the slot-major table
-// (DevKeyTable::gather) into VGPRs: LDS serves only the round tables, so the per-interface
-// key rows cost no LDS cycles and no bank conflicts (the LDS copy of the round-major image,
-// LdsKey, read 11 random 16 B rows per packet: ~3 conflict cycles each).  issue() starts the
-// loads (global address space: vmcnt only, never lgkmcnt); the rounds wait for each row where
-// they use it.  Valid bits come from the LDS copy s_valid.
-struct GatherKey {
-    uint4 k[11];
-    uint32_t slot;
-    __device__ __forceinline__ void issue(const DevKeyTable *tab, uint32_t s)
-    {
-        slot = s;
-        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-        typedef const __attribute__((address_space(1))) v4 *G4;
-        const G4 g = (G4)(tab->gather[s]);   // generic -> global address space
-#pragma unroll
-        for (int j = 0; j < 11; ++j) {
-            const v4 x = g[j];
-            k[j] = make_uint4(x.x, x.y, x.z, x.w);
-        }
-    }
-    __device__ __forceinline__ uint4 row(int r) const { return r == 0 ? k[0] : r == 11 ? k[1] : k[r]; }
-    template <int TAB>
-    __device__ __forceinline__ uint4 rk(int r) const
-    {
-        static_assert(TAB == 4, "gathered rows are not rotated");
-        return k[r];
-    }
-    __device__ __forceinline__ bool ok() const { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
-};
-
-__device__ __forceinline__ void fill_valid(const DevKeyTable *tab)
-{
-    if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
-}
-
 // ---------------------------------------------------------------------------------------
-// Per-interface keys with the round keys of rounds 3..10 expanded per packet (SchedKey).
-// LDS holds only three 16-byte rows per slot -- row 0 (rk0 ^ K1), row 11 (round 1 folded),
-// rk2 -- 12 KiB beside all four round tables, instead of the 48 KiB image beside two: the
-// random-slot ds_read_b128 of a key row costs ~3 conflict cycles per lane group (16 lanes over
-// 16 quad-banks), the four S-box lookups that derive the next round key (aes.c:120-137's
-// schedule step) are conflict-free T-table reads (32 lane copies).  11 -> 3 random rows and no
-// 16-bit rotation per column (the 4-table layout) for 32 extra conflict-free lookups per packet.
-static __shared__ uint4 s_keys3[3 * HFV_MAX_KEYS];
+// Per-interface keys (config 3, KEYSEL_IFID): five 16-byte rows per slot in LDS beside all
+// four round tables -- row 0 (rk0 ^ K1), row 11 (round 1 folded), rk2, and the key-schedule
+// words t_r = SubWord(RotWord(w_{4r-1})) ^ Rcon_r of rounds 3..6 and 7..10 (DevKeyTable::sched,
+// aes.c:120-137) -- 20 KiB for 256 slots.  Round key r then follows from round key r - 1 by
+// XOR alone (w_{4r} = w_{4r-4} ^ t_r, w_{4r+j} = w_{4r+j-4} ^ w_{4r+j-1}): per packet five
+// random-slot ds_read_b128 (each ~3 LDS cycles per 16-lane group: 16 lanes over 16 quad-banks)
+// and no S-box lookup for the schedule.  Round 4 expanded rounds 3..10 per packet from rk2 with
+// four conflict-free T-table reads per step (32 lookups and 16 v_perm per packet, three rows):
+// 186.8 LDS instructions per 64-packet tile against 150.7 for one key.
+constexpr int kSchedRows = 5;
+static __shared__ uint4 s_keys5[kSchedRows * HFV_MAX_KEYS];
 
-__device__ __forceinline__ void fill_keys3(const DevKeyTable *tab, uint32_t nthr)
+__device__ __forceinline__ void fill_keys5(const DevKeyTable *tab, uint32_t nthr)
 {
-    // image rows 0 and 11 as stored; rk2 (image row 2, stored rotated by 16) unrotated
-    for (uint32_t e = threadIdx.x; e < 3 * HFV_MAX_KEYS; e += nthr) {
+    // image rows 0 and 11 as stored; rk2 (image row 2, stored rotated by 16) unrotated; the
+    // two schedule rows as stored
+    for (uint32_t e = threadIdx.x; e < kSchedRows * HFV_MAX_KEYS; e += nthr) {
         const uint32_t j = e / HFV_MAX_KEYS, k = e % HFV_MAX_KEYS;
-        const uint32_t *p = tab->rows[j == 0 ? 0 : j == 1 ? 11 : 2][k];
+        const uint32_t *p = j < 3 ? tab->rows[j == 0 ? 0 : j == 1 ? 11 : 2][k] : tab->sched[j - 3][k];
         uint4 v = make_uint4(p[0], p[1], p[2], p[3]);
         if (j == 2) v = make_uint4(rot16(v.x), rot16(v.y), rot16(v.z), rot16(v.w));
-        s_keys3[e] = v;
+        s_keys5[e] = v;
     }
     if (threadIdx.x < 8) s_valid[threadIdx.x] = tab->valid[threadIdx.x];
 }
 
-// One AES-128 key-schedule step (FIPS-197 5.2; aes.c aes_key_expansion) on the 4-table LDS
-// layout: SubWord(RotWord(w3)) from four T-table reads whose S(x) byte already sits in the
-// output position -- T2[b1] byte 0, T0[b2] byte 1, T1[b3] byte 2, T2[b0] byte 3 -- merged by
-// two v_perm (disjoint bytes, so the xor below joins them).
-__device__ __forceinline__ uint4 next_round_key(const uint4 &rk, uint32_t rcon, const Lane &l)
+// One AES-128 key-schedule step from its precomputed word t = SubWord(RotWord(w3)) ^ Rcon.
+__device__ __forceinline__ uint4 next_round_key(const uint4 &rk, uint32_t t)
 {
-    const uint32_t a = tlu<4, 1>(rk.w, l.b2, l), b = tlu<4, 2>(rk.w, l.b0, l);
-    const uint32_t c = tlu<4, 3>(rk.w, l.b1, l), d = tlu<4, 0>(rk.w, l.b2, l);
-    const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0500u);   // S(b1) | S(b2) << 8
-    const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x07020c0cu);   // S(b3) << 16 | S(b0) << 24
     uint4 n;
-    n.x = xor3(rk.x, lo, hi) ^ rcon;
+    n.x = rk.x ^ t;
     n.y = rk.y ^ n.x;
     n.z = rk.z ^ n.y;
     n.w = rk.w ^ n.z;
     return n;
 }
 
-// Tag words 0..1 of a record-derived macinput for the slot's key (s_keys3 + expansion).
+__device__ __forceinline__ bool slot_valid(uint32_t slot) { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
+
+// Tag words 0..1 of a record-derived macinput for the slot's key (s_keys5).
 __device__ __forceinline__ void cmac48_sched(const uint32_t w[4], uint32_t slot, const Lane &l, uint32_t &t0,
                                              uint32_t &t1)
 {
-    const uint4 k0 = s_keys3[slot];
+    const uint4 k0 = s_keys5[slot];
+    const uint4 r1 = s_keys5[HFV_MAX_KEYS + slot];
+    uint4 rk = s_keys5[2 * HFV_MAX_KEYS + slot];   // rk2
+    const uint4 ta = s_keys5[3 * HFV_MAX_KEYS + slot], tb = s_keys5[4 * HFV_MAX_KEYS + slot];
+    const uint32_t t[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
-    round1_macinput<4>(s, s_keys3[HFV_MAX_KEYS + slot], l);
-    uint4 rk = s_keys3[2 * HFV_MAX_KEYS + slot];   // rk2
+    round1_macinput<4>(s, r1, l);
     round_full<4>(s, rk, l);
-    uint32_t rcon = 0x04u;                         // round 3's (rcon_r = x^(r-1) in GF(2^8))
 #pragma unroll
     for (int r = 3; r < 10; ++r) {
-        rk = next_round_key(rk, rcon, l);
-        rcon = (rcon << 1) ^ ((rcon & 0x80u) ? 0x11bu : 0u);
+        rk = next_round_key(rk, t[r - 3]);
         round_full<4>(s, rk, l);
     }
-    rk = next_round_key(rk, rcon, l);              // rk10, rcon 0x36
+    rk = next_round_key(rk, t[7]);                 // rk10
     round_last_48<4>(s, rk, l, t0, t1);
 }
 

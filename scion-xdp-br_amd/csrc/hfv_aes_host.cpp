@@ -100,6 +100,14 @@ void compile_dev_key(const hop_key *hk, uint32_t dk[4 * kDevKeyRows])
     for (int i = 4; i < 40; ++i) dk[i] = rotl32(dk[i], 16);    // rows 1..9 pre-rotated (hfv_tables.h)
 }
 
+// Key-schedule words of rounds 3..10 (DevKeyTable::sched): t_r = SubWord(RotWord(w[4r-1])) ^
+// Rcon[r] = w[4r] ^ w[4r-4] (aes.c:120-137).
+void compile_dev_sched(const hop_key *hk, uint32_t t[8])
+{
+    const uint32_t *w = hk->key.w;
+    for (int r = 3; r <= 10; ++r) t[r - 3] = w[4 * r] ^ w[4 * r - 4];
+}
+
 }  // namespace hfv
 
 // ---------------------------------------------------------------------------------------

@@ -253,6 +253,7 @@ struct hfv_ctx {
     SvcWeights svc_w_used = svc_w;   // the running / last grid's
     bool svc_adapt = false;          // the running grid got all its batches up front (svc_run): measure it
     std::vector<uint64_t> svc_run_ns;   // ... their record counts
+    struct timespec svc_launch_ts = {0, 0};   // host clock at the running grid's launch call
 };
 
 static int device_numa(int device, cpu_set_t *cpus);
@@ -326,21 +327,18 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         int next = ctx->active ^ 1;
         // wait (host) until the previous copy out of the staging image has been consumed
         HIP_TRY(hipEventSynchronize(ctx->img_free));
-        // the slot-major copy only for the service's gather variant (HFV_SVC_IFID=gather), the
-        // only reader: 64 KiB less per publish otherwise
-        static const bool gather = getenv("HFV_SVC_IFID") && !strcmp(getenv("HFV_SVC_IFID"), "gather");
         for (uint32_t k = 0; k < HFV_MAX_KEYS; ++k) {
-            uint32_t dk[4 * kDevKeyRows];
-            if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) compile_dev_key(&ctx->shadow[k], dk);
-            else memset(dk, 0, sizeof dk);
+            uint32_t dk[4 * kDevKeyRows], t[8];
+            if ((ctx->valid[k >> 5] >> (k & 31)) & 1u) {
+                compile_dev_key(&ctx->shadow[k], dk);
+                compile_dev_sched(&ctx->shadow[k], t);
+            } else {
+                memset(dk, 0, sizeof dk);
+                memset(t, 0, sizeof t);
+            }
             for (int r = 0; r < kDevKeyRows; ++r) memcpy(ctx->host_img->keys.rows[r][k], dk + 4 * r, 16);
-            if (!gather) continue;
-            uint32_t(*g)[4] = ctx->host_img->keys.gather[k];   // slot-major, rows 2..9 unrotated
-            memcpy(g[0], dk, 16);
-            memcpy(g[1], dk + 44, 16);
-            for (int r = 2; r < 10; ++r)
-                for (int c = 0; c < 4; ++c) g[r][c] = (dk[4 * r + c] << 16) | (dk[4 * r + c] >> 16);
-            memcpy(g[10], dk + 40, 16);
+            memcpy(ctx->host_img->keys.sched[0][k], t, 16);
+            memcpy(ctx->host_img->keys.sched[1][k], t + 4, 16);
         }
         memcpy(ctx->host_img->keys.valid, ctx->valid, sizeof ctx->valid);
         ctx->host_img->br = ctx->br;
@@ -362,14 +360,7 @@ static int publish_keys(hfv_ctx *ctx, hipStream_t st, DevState **out)
         ctx->nreaders[next] = 0;
         ctx->readers_overflow[next] = false;
         if (g_pub_delay_us) HIP_TRY((hipError_t)launch_debug_spin(st, g_pub_delay_us));
-        if (gather) {
-            HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
-        } else {   // the key rows and valid bits, then the router tables (the gather rows stay unused)
-            HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, offsetof(DevKeyTable, gather),
-                                   hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(&ctx->dev_tab[next]->br, &ctx->host_img->br, sizeof(DevBrConfig),
-                                   hipMemcpyHostToDevice, st));
-        }
+        HIP_TRY(hipMemcpyAsync(ctx->dev_tab[next], ctx->host_img, sizeof(DevState), hipMemcpyHostToDevice, st));
         HIP_TRY(hipEventRecord(ctx->img_free, st));
         ctx->active = next;
         ctx->dirty = false;
@@ -451,12 +442,8 @@ int hfv_ctx_create(int device, hfv_ctx **out)
         if (rc) break;
         if (query_geometry(device, &c->geom) != 0) {
             hfv_ctx_destroy(c);
-            return fail(-EINVAL, "no kernel variant matches HFV_KVARIANT / HFV_KVARIANT_IFID");
+            return fail(-EINVAL, "device %d cannot hold a 1024-thread verify block with 156 KiB of LDS", device);
         }
-        uint32_t *img = nullptr;
-        if (hipMalloc((void **)&img, kTtabImageDwords * 4) != hipSuccess) { rc = -ENOMEM; break; }
-        c->geom.ttab_img = img;
-        if (build_ttab_image(img, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess) { rc = -EIO; break; }
     } while (0);
     if (rc) {
         hfv_ctx_destroy(c);
@@ -506,7 +493,6 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     if (ctx->img_free) { (void)hipEventSynchronize(ctx->img_free); (void)hipEventDestroy(ctx->img_free); }
     if (ctx->host_img) (void)hipHostFree(ctx->host_img);
-    if (ctx->geom.ttab_img) (void)hipFree((void *)ctx->geom.ttab_img);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -711,7 +697,7 @@ extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
     const DevKeyTable *tab = &ds->keys;
-    uint64_t tiles = (n + 63) / 64, blocks = (tiles + 15) / 16, cap = (uint64_t)ctx->geom.num_cus * ctx->geom.single.blocks_per_cu;
+    uint64_t tiles = (n + 63) / 64, blocks = (tiles + 15) / 16, cap = (uint64_t)ctx->geom.num_cus;
     *grid = (int)(blocks < cap ? blocks : cap);
     int e = launch_verify_stamped(ctx->geom, tab, &ctx->host_img->keys, (const uint8_t *)recs, n, pass_bits, stamps, st);
     return after_launch(ctx, st, e, "stamped launch");
@@ -720,16 +706,11 @@ extern "C" int hfv_debug_verify_stamped(hfv_ctx *ctx, const void *recs, size_t n
 int hfv_ctx_describe(const hfv_ctx *ctx, char *buf, size_t len)
 {
     if (!ctx || !buf || !len) return fail(-EINVAL, "null argument");
-    const KernelVariant &a = ctx->geom.single, &b = ctx->geom.multi;
-    // the resident service's per-interface key layout (launch_service, hfv_kernels.hip)
-    const char *iv = getenv("HFV_SVC_IFID");
-    const char *svc_ifid = iv && !strcmp(iv, "gather") ? "gather" : iv && !strcmp(iv, "lds") ? "lds" : "sched";
     snprintf(buf, len,
-             "zero: block=%d pf=%d tab=%d dma=%d np=%d dyn=%d bs=%d grid=%dx%d; ifid: block=%d pf=%d tab=%d dma=%d "
-             "np=%d dyn=%d grid=%dx%d; service ifid keys=%s tab=%d",
-             a.block, a.pf, a.tab, a.dma, a.np, a.dyn, a.bs, ctx->geom.num_cus, a.blocks_per_cu, b.block, b.pf, b.tab,
-             b.dma,
-             b.np, b.dyn, ctx->geom.num_cus, b.blocks_per_cu, svc_ifid, strcmp(svc_ifid, "lds") ? 4 : 2);
+             "verify: 1024-thread blocks, one per CU (%d CUs), four 32x-replicated round tables in LDS (128 KiB), "
+             "T0 and slot-0 key rows in the kernel arguments; keysel ifid: five 16 B LDS rows per slot "
+             "(round-1 folded key, rk2, schedule words of rounds 3..10); service grid %d blocks",
+             ctx->geom.num_cus, ctx->geom.svc_blocks);
     return 0;
 }
 
@@ -1612,15 +1593,18 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
 // time from table fill to its last completed share is its verify rate).  Weights follow the
 // XCDs' mean rates (block j on XCD j % 8) and block 0's own, averaged with the previous weights
 // (halves run-to-run noise), clamped to [1/2, 2] of nominal.  Grids shorter than 50 us carry
-// too little signal and leave them alone.  HFV_SVC_BALANCE=0 keeps equal shares.
-static void svc_balance(hfv_ctx *ctx)
+// too little signal and leave them alone: with the grid's wall time from the host's clock
+// (ns) below that, the stamps are not even copied (a synchronous 16 KiB copy after
+// every short grid).
+static void svc_balance(hfv_ctx *ctx, double grid_ns)
 {
-    static const bool off = getenv("HFV_SVC_BALANCE") && !strcmp(getenv("HFV_SVC_BALANCE"), "0");
     const uint64_t G = ctx->svc_grid;
-    if (off || G < 16 || ctx->svc_run_ns.empty()) return;
-    std::vector<uint64_t> bt(2 * kSvcMaxBlocks);   // blk_start[], blk_fin[] (adjacent in SvcDev)
+    if (G < 16 || ctx->svc_run_ns.empty() || grid_ns < 50000.0) return;
+    std::vector<uint64_t> bt(2 * kSvcMaxBlocks);   // blk_start[0..G), blk_fin[0..G) (adjacent in SvcDev)
     static_assert(offsetof(SvcDev, blk_fin) == offsetof(SvcDev, blk_start) + kSvcMaxBlocks * 8, "layout");
-    if (svc_dev_read(ctx, bt.data(), offsetof(SvcDev, blk_start), bt.size() * 8)) return;
+    if (svc_dev_read(ctx, bt.data(), offsetof(SvcDev, blk_start), G * 8) ||
+        svc_dev_read(ctx, bt.data() + kSvcMaxBlocks, offsetof(SvcDev, blk_fin), G * 8))
+        return;
     const uint64_t *blk_start = bt.data(), *blk_fin = bt.data() + kSvcMaxBlocks;
     const SvcWeights &wu = ctx->svc_w_used;
     std::vector<uint64_t> cum(G + 1, 0);
@@ -1704,7 +1688,11 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     if (e != hipSuccess) return hip_fail(e, "verify service");
     if (rc) return rc;
     if (kernel_ms && ctx->svc_timed) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
-    if (ctx->svc_adapt && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) svc_balance(ctx);
+    if (ctx->svc_adapt && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) {
+        struct timespec t1;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        svc_balance(ctx, (t1.tv_sec - ctx->svc_launch_ts.tv_sec) * 1e9 + (t1.tv_nsec - ctx->svc_launch_ts.tv_nsec));
+    }
     ctx->svc_adapt = false;
     // A grid that left on the stop descriptor verified every batch before it (each block
     // reaches the stop only after its share of all earlier batches).  An idle or watchdog
@@ -1794,7 +1782,6 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     SvcArgs a;
     memset(&a, 0, sizeof a);
     a.tab = &ds->keys;
-    a.ttab_img = ctx->geom.ttab_img;
     a.host = ctx->svc_host_dev;
     a.dev = ctx->svc_dev;
     a.inf_off = ctx->inf_off;
@@ -1822,6 +1809,7 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     if (rc) return rc;
     ++ctx->svc_launches;
     ctx->svc_running = true;
+    clock_gettime(CLOCK_MONOTONIC, &ctx->svc_launch_ts);   // bounds the grid's life from above (svc_balance)
     return 0;
 }
 
@@ -1942,8 +1930,6 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
                    float *kernel_ms, bool wait)
 {
     if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
-    struct timespec t_in, t_chk, t_beg;
-    clock_gettime(CLOCK_MONOTONIC, &t_in);
     *first_ticket = 0;
     if (kernel_ms) *kernel_ms = 0.0f;
     for (size_t i = 0; i < count; ++i) {
@@ -1957,14 +1943,12 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
     DeviceGuard g(ctx->device);
     int rc = svc_quiesce(ctx);
     if (rc) return rc;
-    clock_gettime(CLOCK_MONOTONIC, &t_chk);
     DevState *ds;
     rc = svc_begin(ctx, ctx->svc_idle_ms, &ds);
     if (rc) return rc;
     ctx->svc_adapt = true;   // every batch is in the ring before the grid starts: measure its balance
     ctx->svc_run_ns.resize(count);
     for (size_t i = 0; i < count; ++i) ctx->svc_run_ns[i] = batches[i].n;
-    clock_gettime(CLOCK_MONOTONIC, &t_beg);
     // the batches, then the stop right behind them, are in the ring before the grid starts (a
     // longer run launches once the ring is full): the grid exits as soon as its blocks finish
     // their share of the last batch, with no stop to post and relay afterwards
@@ -1985,32 +1969,12 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
                       batches[i].n, batches[i].stride, &t);
         if (i == 0) *first_ticket = t;
     }
-    struct timespec t_post, t_launch, t_done;
-    clock_gettime(CLOCK_MONOTONIC, &t_post);
     if (!launched) {
         int lr = svc_launch(ctx, ds);
         if (lr) return lr;
     }
-    clock_gettime(CLOCK_MONOTONIC, &t_launch);
-    static const bool trace = getenv("HFV_SVC_TRACE") != nullptr;   // diagnostics
-    auto us = [](const timespec &a, const timespec &b) {
-        return (b.tv_sec - a.tv_sec) * 1e6 + (b.tv_nsec - a.tv_nsec) / 1e3;
-    };
-    if (!wait) {   // the grid exits after the stop posted behind the batches
-        if (trace)
-            fprintf(stderr, "hfv_service_run_async: checks+guard+quiesce %.1f us, begin %.1f us, posts %.1f us, "
-                    "launch call %.1f us\n", us(t_in, t_chk), us(t_chk, t_beg), us(t_beg, t_post), us(t_post, t_launch));
-        return rc;
-    }
+    if (!wait) return rc;   // the grid exits after the stop posted behind the batches
     int sr = svc_stop(ctx, kernel_ms);
-    clock_gettime(CLOCK_MONOTONIC, &t_done);
-    if (trace) {
-        fprintf(stderr,
-                "hfv_service_run: checks+guard+quiesce %.1f us, begin %.1f us, posts %.1f us, launch call %.1f us, "
-                "launch return -> grid exit seen %.1f us, grid %.1f us\n",
-                us(t_in, t_chk), us(t_chk, t_beg), us(t_beg, t_post), us(t_post, t_launch), us(t_launch, t_done),
-                kernel_ms ? *kernel_ms * 1e3 : -1.0);
-    }
     return rc ? rc : sr;
 }
 
@@ -2018,6 +1982,15 @@ int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     int st = svc_ticket_state(ctx, ticket);
+    if (st == 0 && ctx->svc_running && hipStreamQuery(ctx->svc_stream) == hipSuccess) {
+        // The grid is gone without its stop (idle timeout or watchdog): its relay wave stopped
+        // forwarding completions when it published the stop, so the host ring may never show
+        // this ticket.  Reap the grid: svc_stop reads the device completion words and records
+        // the tickets it left unverified (a poll loop never ended).
+        DeviceGuard g(ctx->device);
+        (void)svc_stop(ctx, nullptr);
+        st = svc_ticket_state(ctx, ticket);
+    }
     if (st == -EINVAL) return fail(-EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
     if (st == -EIO) return fail(-EIO, "verify service stopped before ticket %llu", (unsigned long long)ticket);
     return st;
@@ -2050,6 +2023,16 @@ int hfv_service_set_timing(hfv_ctx *ctx, int enable)
     return 0;
 }
 
+int hfv_service_set_grid(hfv_ctx *ctx, int blocks)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    if (blocks < 0) return fail(-EINVAL, "blocks %d < 0", blocks);
+    DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);   // the next grid takes the new shape
+    ctx->geom.svc_blocks = blocks == 0 || blocks > ctx->geom.num_cus ? ctx->geom.num_cus : blocks;
+    return 0;
+}
+
 // Diagnostic (not part of include/scion_hfv.h): the block weights the next service grid will
 // use (w[0..7] per XCD, then block 0's), in units of 1/1024 of an equal share.
 int hfv_debug_service_weights(hfv_ctx *ctx, uint32_t out[9])
@@ -2058,20 +2041,6 @@ int hfv_debug_service_weights(hfv_ctx *ctx, uint32_t out[9])
     for (int x = 0; x < 8; ++x) out[x] = ctx->svc_w.w[x];
     out[8] = ctx->svc_w.w0;
     return 0;
-}
-
-// Diagnostic (not part of include/scion_hfv.h; HFV_SVC_SPAN builds fill it): the last grid's
-// block entry stamps (grid words), table-fill stamps (grid words) and wave exit stamps (grid *
-// 16 words, block * 16 + wave; 0 for a wave that did not run the loop), s_memrealtime (100 MHz).
-int hfv_debug_service_span(hfv_ctx *ctx, uint64_t *out, size_t words)
-{
-    if (!ctx || !out || !ctx->svc_dev) return fail(-EINVAL, "bad argument");
-    const size_t g = ctx->svc_grid;
-    if (words < g * 18) return fail(-EINVAL, "need %zu words", g * 18);
-    int rc = svc_dev_read(ctx, out, offsetof(SvcDev, span_entry), g * 8);
-    if (!rc) rc = svc_dev_read(ctx, out + g, offsetof(SvcDev, span_fill), g * 8);
-    if (!rc) rc = svc_dev_read(ctx, out + 2 * g, offsetof(SvcDev, span_exit), g * 16 * 8);
-    return rc;
 }
 
 // Diagnostic (not part of include/scion_hfv.h): out[i] = s_memrealtime (100 MHz) when block
@@ -2121,20 +2090,36 @@ int hfv_debug_service_relay(hfv_ctx *ctx, uint64_t out[8])
     return rc;
 }
 
+// Diagnostic (not part of include/scion_hfv.h): INTEGRATION.md section 2's data-plane loop,
+// timed -- per RX batch one hfv_service_submit, then hfv_service_wait on the ticket `depth`
+// batches back (a feeder keeping `depth` batches in flight), the last tickets at the end; *ns =
+// host nanoseconds from the first submit to the last wait's return.  The same public calls a C
+// maintainer writes, without a foreign-function layer in between (bench.py's `per_call` leg).
+int hfv_debug_feed_loop(hfv_ctx *ctx, const struct hfv_batch *b, size_t count, uint32_t depth, uint64_t *ns)
+{
+    if (!ctx || !ns || (!b && count) || depth == 0) return fail(-EINVAL, "bad argument");
+    std::vector<uint64_t> t(count);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (size_t i = 0; i < count; ++i) {
+        int rc = hfv_service_submit(ctx, b[i].recs, b[i].stride, b[i].n, b[i].pass_bits, &t[i]);
+        if (!rc && i >= depth) rc = hfv_service_wait(ctx, t[i - depth], 10000);
+        if (rc) return rc;
+    }
+    for (size_t i = count > depth ? count - depth : 0; i < count; ++i) {
+        int rc = hfv_service_wait(ctx, t[i], 10000);
+        if (rc) return rc;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    *ns = (uint64_t)((t1.tv_sec - t0.tv_sec) * 1000000000ll + (t1.tv_nsec - t0.tv_nsec));
+    return 0;
+}
+
 // Test hook (not part of include/scion_hfv.h): every host read of later service grids' relay
 // wave takes `us` microseconds longer (a slow PCIe link), 0 = off.
 int hfv_debug_relay_delay(uint32_t us)
 {
     g_svc_relay_delay_us = us > 100000u ? 100000u : us;
-    return 0;
-}
-
-// Diagnostic: the HFV_SVC_PROF phase counters (SvcShared::prof) summed over all grids since
-// the last call, then cleared.
-extern "C" int hfv_debug_service_prof(hfv_ctx *ctx, uint64_t *out8)
-{
-    if (!ctx || !out8 || !ctx->svc_host) return fail(-EINVAL, "bad argument");
-    for (int i = 0; i < 8; ++i) out8[i] = __atomic_exchange_n(&ctx->svc_host->prof[i], 0, __ATOMIC_ACQ_REL);
     return 0;
 }
 

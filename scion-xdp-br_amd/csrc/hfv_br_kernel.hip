@@ -1021,12 +1021,10 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     // SegID store can overwrite are kept before it, keep_mac_bytes), so reading `pkts` while
     // writing `out` gives the in-place result.
     if (!out) out = pkts;
-    // Staged variant when the 16-byte header loads are aligned and in bounds (HFV_BR_STAGE=0
-    // forces the direct one).  Persistent grid: one block per CU (LDS: tables + counters
-    // [+ header rows]).
-    static const int stage_env = getenv("HFV_BR_STAGE") ? atoi(getenv("HFV_BR_STAGE")) : 1;
+    // Staged variant when the 16-byte header loads are aligned and in bounds, the direct one
+    // otherwise.  Persistent grid: one block per CU (LDS: tables + counters [+ header rows]).
     // (the staged loop addresses a tile of 64 slots through 32-bit buffer offsets: 64 * slot < 2^31)
-    bool staged = stage_env && slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0 &&
+    bool staged = slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0 &&
                   ((uintptr_t)out & 15) == 0 && slot < ((size_t)1 << 25);
     using K = void (*)(const DevState *, const uint32_t *, const uint8_t *, uint8_t *, uint64_t, uint32_t, uint32_t,
                        const uint16_t *,
@@ -1066,7 +1064,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
     if (g_br_grid_override && g_br_grid_override < grid) grid = g_br_grid_override;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)g.ttab_img, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)nullptr, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
                           (unsigned long long *)stats);
     return (int)hipGetLastError();

@@ -19,19 +19,19 @@ void hop_key_from_key(const uint8_t key[16], hop_key *hk);
 void compile_dev_key(const hop_key *hk, uint32_t dk[4 * kDevKeyRows]);
 
 // Device key table as the kernels see it: dev keys in round-major order
-// [kDevKeyRows][HFV_MAX_KEYS] x 16 B, followed by the 256-bit valid bitmap.
-constexpr int kGatherRows = 16;   // 11 used: one slot = 256 B = two 128 B lines
+// [kDevKeyRows][HFV_MAX_KEYS] x 16 B, the 256-bit valid bitmap, then the key-schedule words of
+// rounds 3..10 per slot for the per-interface-key kernels (config 3): sched[0][k] = t3..t6,
+// sched[1][k] = t7..t10, t_r = SubWord(RotWord(w_{4r-1})) ^ Rcon_r = w_{4r} ^ w_{4r-4}
+// (aes.c:120-137), so that round key r follows from round key r - 1 by XOR alone.
 struct DevKeyTable {
     uint32_t rows[kDevKeyRows][HFV_MAX_KEYS][4];
     uint32_t valid[8];
-    uint32_t pad_[56];   // gather[] on a 256 B boundary
-    // Slot-major copy for the kernels that gather each packet's key rows into VGPRs
-    // (per-interface keys with the 4-table layout, hfv_aes_dev.h GatherKey): gather[slot][j],
-    // j = 0: row 0 (rk0 ^ K1), 1: row 11 (folded round 1), 2..9: rounds 2..9 NOT rotated,
-    // 10: row 10 (last round); 11..15 unused.
-    uint32_t gather[HFV_MAX_KEYS][kGatherRows][4];
+    uint32_t pad_[24];
+    uint32_t sched[2][HFV_MAX_KEYS][4];
 };
-static_assert(offsetof(DevKeyTable, gather) % 256 == 0, "gather rows on 256 B boundaries");
+static_assert(offsetof(DevKeyTable, sched) % 128 == 0, "schedule rows on 128 B boundaries");
+// the schedule words of a hop_key (host side of DevKeyTable::sched)
+void compile_dev_sched(const hop_key *hk, uint32_t t[8]);
 
 // Router tables as the config-4 kernel sees them (compiled from struct hfv_br_config by
 // hfv_br_set_config).  Addresses/ports keep the BPF code's little-endian view of wire bytes
@@ -111,7 +111,8 @@ enum KernelMode { kModeRecords = 0, kModeMacinputs = 1, kModeTags = 2 };
 // complete, which is what lets each block cache kSvcRing descriptors in LDS without any reuse
 // check (hfv_kernels.hip, k_verify_service).  A grid that exits on its stop descriptor has
 // verified every batch before it, so the host needs no forwarded completion for those.
-constexpr uint32_t kSvcRing = 256;   // batches in flight (a host hiccup of ~3 ms at 2^20 records does not starve the grid)
+constexpr uint32_t kSvcRing = 128;   // batches in flight (a host hiccup of ~1.5 ms at 2^20 records does not starve the grid;
+                                     // 128 x 64 B of descriptor cache per block leaves LDS room for config 3's key rows)
 constexpr uint32_t kSvcMaxBlocks = 1024;
 constexpr uint32_t kSvcInline = 64;  // descriptors in the kernel arguments
 constexpr uint64_t kSvcStopN = ~0ull;   // descriptor n: the service exits
@@ -125,7 +126,6 @@ struct SvcShared {   // pinned host memory
     uint64_t status;                 // nonzero: the grid stopped on its own (kSvcIdleTimeout, kSvcWatchdog)
     uint64_t pad[7];
     uint64_t done[kSvcRing];         // done[(t-1) % kSvcRing] = tag | t: batch t verified (forwarded by the relay)
-    uint64_t prof[8];                // diagnostics (HFV_SVC_PROF builds): shader cycles per loop phase, summed over waves
 };
 // Relay diagnostics (SvcDev::relay), one grid's worth: how the host link behaved for it.
 enum SvcRelayStat {
@@ -158,35 +158,18 @@ struct SvcDev {   // device memory: written by the grid; the host copies what it
     // s_memtime (shader clock) at the same two points: each block's clock over its loop
     uint64_t blk_clk0[kSvcMaxBlocks];
     uint64_t blk_clk1[kSvcMaxBlocks];
-    // HFV_SVC_SPAN builds: s_memrealtime at each block's entry and after its table fill, and at
-    // each wave's exit (block * 16 + wave)
-    uint64_t span_entry[kSvcMaxBlocks];
-    uint64_t span_fill[kSvcMaxBlocks];
-    uint64_t span_exit[kSvcMaxBlocks * 16];
     SvcArea area[2];
     uint64_t done[kSvcRing][kSvcMaxBlocks];   // done[(t-1) % kSvcRing][k] = tag | t: block k's share of t is verified
 };
 constexpr uint64_t kSvcIdleTimeout = 2;
 constexpr uint64_t kSvcWatchdog = 3;    // a wave gave up waiting for its block's loader
 
-struct KernelVariant {
-    int block;           // threads per block
-    int pf;              // record tiles loaded ahead of the one computed (1 or 2)
-    int tab;             // round tables in LDS: 2 (T0/T1, 64 KiB) or 4 (T0..T3, 128 KiB)
-    int blocks_per_cu;   // persistent grid = num_cus * blocks_per_cu
-    int dma;             // 1: fill the LDS tables from ttab_img by LDS-DMA; 0: compute them
-    int np;              // packets per lane computed together (1 or 2)
-    int dyn;             // 1: waves pull tiles from a per-block LDS queue; 0: static stride
-    int bs;              // KEYSEL_ZERO only: 0 T-table waves only; 1..4 bitsliced waves per
-                         // block beside the T-table waves (hybrid); kBsOnly all bitsliced
-};
-constexpr int kBsOnly = 99;
-
+// Launch geometry of the one-launch-per-batch verify kernels: a persistent grid of one
+// 1024-thread block per CU (LDS: the four 32x-replicated round tables, 128 KiB, plus config 3's
+// 20 KiB of key rows), fixed at build time; the resident service takes the same shape.
 struct LaunchGeom {
     int num_cus;
-    KernelVariant single;   // KEYSEL_ZERO record verify
-    KernelVariant multi;    // KEYSEL_IFID record verify (per-lane keys in LDS)
-    const uint32_t *ttab_img;   // 16 KiB compact source of the replicated T0..T3 LDS tables (k_build_ttab_image)
+    int svc_blocks;   // blocks of a service grid: num_cus, or fewer (hfv_service_set_grid)
 };
 
 // kernel launchers (hfv_kernels.hip); return hipError_t as int
@@ -220,8 +203,6 @@ int query_geometry(int device, LaunchGeom *g);
 int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, const uint8_t *recs,
                           size_t n,
                           uint64_t *bits, uint64_t *stamps, void *stream);
-constexpr uint32_t kTtabImageDwords = 4096;   // 1024 entries x 16 B
-int build_ttab_image(uint32_t *img, void *stream);
 // persistent verify service (one block of 1024 threads per CU); idle_ticks: 100 MHz ticks a
 // block waits for the next descriptor before it exits with status kSvcIdleTimeout
 // returns the grid size in *grid
@@ -255,7 +236,6 @@ constexpr uint64_t svc_cum(const SvcWeights &sw, uint64_t k)
 // inline descriptors straight from the kernarg segment, indexed by batch).
 struct SvcArgs {
     const DevKeyTable *tab;
-    const uint32_t *ttab_img;
     SvcShared *host;   // device view of the pinned ring
     SvcDev *dev;
     uint32_t inf_off, hf_off;
@@ -273,6 +253,9 @@ struct SvcArgs {
     uint32_t t0[256];
     SvcDescLite inl[kSvcInline];
 };
+// both travel as one by-value kernel argument: the kernarg segment holds at most 4 KiB
+static_assert(sizeof(SvcArgs) <= 4096, "SvcArgs exceeds the 4 KiB kernel-argument segment");
+static_assert(sizeof(RecArgs) + 128 <= 4096, "RecArgs and the launch's other arguments exceed 4 KiB");
 int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid);
 // full border-router path (hfv_br_kernel.hip)

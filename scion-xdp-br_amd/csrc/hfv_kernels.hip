@@ -4,18 +4,24 @@
 // aes_cypher (br/src/bpf/xdp.c:77-91, aes/include/aes/aes.h:129-141, aes/src/aes.c:249-293)
 // with one lane per packet:
 //
-//   * AES round tables live in LDS, replicated 32x so that lane L always reads copy L%32:
-//     dword (x << 6) | (t << 5) | (L & 31) holds table t (0 = T0, 1 = T1 = rotl8(T0)) at
-//     index x.  ds_read_b32 banks are (addr/4) % 32 over each 32-lane half, so every
-//     lookup is bank-conflict free whatever the data.  T2/T3 are T0/T1 rotated by 16 and
-//     are folded in with one v_alignbit per column.
+//   * The four AES round tables T0..T3 live in LDS (128 KiB), replicated 32x so that lane L
+//     always reads copy L%32: byte address (x << 8) | (t&1) << 7 | (L&31) << 2 | (t>>1) << 16
+//     holds table t at index x.  ds_read_b32 banks are (addr/4) % 32 over each 32-lane half,
+//     so every lookup is bank-conflict free whatever the data (hfv_aes_dev.h).
 //   * The LDS byte address of a lookup is built with ONE v_perm_b32: byte 1 <- the state
-//     byte, byte 0 <- the lane's copy/table bits, bytes 2-3 <- 0.
+//     byte, byte 0 <- the lane's copy/table bits, byte 2 <- the T2/T3 bit.
 //   * Round keys: a single key (KEYSEL_ZERO, the reference rule xdp.c:82) is wave-uniform
-//     and stays in SGPRs; per-packet keys come from an LDS copy of the key table.
-//   * Verdicts: one __ballot per wave = 64 pass bits, one 8-byte store by lane 0.
-//   * Persistent grid (a few blocks per CU) so the 64 KiB table fill is paid once per
-//     block; the next tile's record bytes are prefetched while the current tile computes.
+//     and stays in SGPRs; per-interface keys (KEYSEL_IFID, config 3) come from five 16-byte
+//     LDS rows per slot, the schedule words of rounds 3..10 precomputed (hfv_aes_dev.h).
+//   * Verdicts: one __ballot per wave = 64 pass bits per 64 records.
+//   * Persistent grid of one 1024-thread block per CU, so the table fill is paid once per
+//     block; the next tile's record bytes are loaded while the current tile computes.
+//
+// Rejected variants measured in rounds 1-4 (bitsliced and hybrid AES, LDS-DMA and VGPR table
+// fills, per-lane key rows gathered from L2, the 48 KiB key image beside two tables, two
+// packets per lane, 2 blocks per CU) are documented in DESIGN.md and profiles/ab_index.md;
+// their code is in the history (commit c3ddbb7).  Nothing read from the environment selects a
+// kernel.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,44 +30,9 @@
 #include <hip/hip_ext.h>
 
 #include "hfv_aes_dev.h"
-#include "hfv_bitslice.h"
 #include "hfv_internal.h"
 
 namespace hfv {
-
-// How the one-launch-per-batch kernel fills its LDS round tables: 3 (default) from T0 in its
-// kernel arguments (RecArgs: the block prologue is one memory hop, the kernarg segment, with the
-// slot-0 key rows alongside); 2 the compact image copied through VGPRs, its pieces issued
-// before the first tile's records (TtabRegs); 1 LDS-DMA from the compact image after the
-// records.  The resident service takes T0 and the key rows from its arguments too
-// (HFV_SVC_FILL_DMA=1: LDS-DMA).  Measured round 4 (profiles/r04/fill_ab.log, span probe):
-// the service's block prologue (entry -> fill barrier) took 4.1-4.5 us with the key rows and
-// the LDS-DMA source behind a second hop (the 16 KiB compact image or round 3's 128 KiB: the
-// same), 3.4 us with the keys in the arguments and LDS-DMA, 3.0 us with both in the arguments;
-// 5.3 us with the tables computed in the block (GF(2^8) inversion in VALU; removed).
-#ifndef HFV_FILL
-#define HFV_FILL 3
-#endif
-// HFV_SVC_FILL_DMA = 1: the service fills its tables by LDS-DMA from the compact image (a second
-// memory hop after the kernel arguments) instead of from T0 in its kernel arguments
-#ifndef HFV_SVC_FILL_DMA
-#define HFV_SVC_FILL_DMA 0
-#endif
-
-// Compact source of the LDS round tables (the fill_ttab_dma source), built once per ctx:
-// 16 KiB, entry e (16 bytes = 4 copies of one table value) for the 128-byte run of LDS
-// (32 lane copies of table t at index x) that starts at byte e * 128 of the LDS image.  Every
-// lane of an LDS-DMA instruction fetches its 16 bytes from entry (LDS offset / 128), so a
-// block moves 16 KiB from L2 instead of a 128 KiB replicated image (ttab_src, hfv_aes_dev.h).
-__global__ void k_build_ttab_image(uint32_t *__restrict__ img)
-{
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int)kTtabImageDwords) return;
-    const int e = i >> 2;
-    const uint32_t t0 = c_t0[(e >> 1) & 255];
-    const int t = (e & 1) | (((e >> 9) & 1) << 1);
-    img[i] = t ? __builtin_amdgcn_alignbit(t0, t0, 32 - 8 * t) : t0;
-}
 
 // ---------------------------------------------------------------------------------------
 // record verify: macinput from INF/HF (path_processing.h:39-81), CMAC, 48-bit compare
@@ -79,50 +50,21 @@ struct RecWords {
 
 // Unconditional loads (no branch around them, so the compiler can keep a counted vmcnt for
 // the prefetch): lanes past the end re-read the last record and are masked off later.
-// NT: non-temporal loads (records are read once per launch).  The resident service uses
-// plain, cache-allocating loads instead: a batch re-posted from the same ring slots (the
-// benchmark re-verifies one resident 64 MiB batch) is then served from the Infinity Cache
-// (measured at 2^20: +8-10 %; neutral at 2^24, where the batch does not fit).
-template <bool NT = true>
+// Non-temporal: the records are read once per launch.
 __device__ __forceinline__ RecWords load_rec(const uint8_t *recs, uint64_t stride, uint64_t i, uint64_t last,
                                              uint32_t inf_off, uint32_t hf_off)
 {
     RecWords r;
-    // global address space even when `recs` came out of memory (the service's descriptors),
-    // so these are global_load (vmcnt only), not flat loads that also count in lgkmcnt
+    // global address space, so these are global_load (vmcnt only), not flat loads that also
+    // count in lgkmcnt
     const GlobalU8 *p = (const GlobalU8 *)(recs) + (i < last ? i : last) * stride;
     typedef const __attribute__((address_space(1))) u32x2 *P2;
     typedef const __attribute__((address_space(1))) uint32_t *P1;
-    u32x2 a, b;
-    if constexpr (NT) {
-        a = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
-        b = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
-        r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
-    } else {
-        a = *reinterpret_cast<P2>(p + inf_off);
-        b = *reinterpret_cast<P2>(p + hf_off);
-        r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
-    }
+    const u32x2 a = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
+    const u32x2 b = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
+    r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
-    return r;
-}
-
-// Same words read with system-scope (L1/L2-bypassing, coherent) loads: what the resident
-// service uses when it may not invalidate the caches per batch (HFV_SVC_ACQ == 2).
-__device__ __forceinline__ RecWords load_rec_sys(const uint8_t *recs, uint64_t stride, uint64_t i, uint64_t last,
-                                                 uint32_t inf_off, uint32_t hf_off)
-{
-    RecWords r;
-    const uint8_t *p = recs + (i < last ? i : last) * stride;
-    uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p + inf_off), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-    uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p + hf_off), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-    r.inf = make_uint2((uint32_t)a, (uint32_t)(a >> 32));
-    r.hfa = make_uint2((uint32_t)b, (uint32_t)(b >> 32));
-    r.hfb = __hip_atomic_load(reinterpret_cast<const uint32_t *>(p + hf_off + 8), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_SYSTEM);
     return r;
 }
 
@@ -150,187 +92,118 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
     return t0 == e0 && ((t1 ^ e1) & 0xffffu) == 0;
 }
 
-// One tile = 64 consecutive records = one wave.  A wave computes NP tiles at once (NP
-// independent AES chains per lane, interleaved by the scheduler to hide LDS latency), and
-// loads its next NP tiles while it computes the current ones (PF = prefetch depth in
-// iterations).  Tiles of one wave: t, t + nwaves, t + 2*nwaves, ...
-// RET = 1: return the ballots in ret[] instead of storing them (the resident service
-// batches its verdict stores).
-template <int KEYSEL, int TAB, int NP, int RET = 0>
-__device__ __forceinline__ void verify_tiles(const RecWords (&cur)[NP], uint64_t t, uint64_t nwaves, uint64_t n,
-                                             uint32_t lane, const Lane &l, const UniformKey *ukey,
-                                             uint64_t *__restrict__ bits, uint64_t *ret = nullptr)
+// One tile = 64 records = one wave: the verdict ballot (bit L = record L of the tile passed).
+// `in`: this lane's record exists.  KEYSEL_ZERO: the wave-uniform slot-0 key (the caller
+// handles an empty slot 0); KEYSEL_IFID: the slot's LDS rows, an empty slot fails closed
+// (xdp.c:83-84).
+template <int KEYSEL>
+__device__ __forceinline__ uint64_t verify_tile(const RecWords &r, bool in, const Lane &l, const UniformKey *ukey)
 {
-    uint32_t s[NP][4];
-    uint32_t slot[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        uint32_t w[4];
-        rec_macinput(cur[p], w);
-        slot[p] = rec_key_slot(cur[p]);
-        uint4 k0;
-        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) k0 = ukey->row(0);
-        else k0 = LdsKey(slot[p]).row(0);
-        s[p][0] = w[0] ^ k0.x; s[p][1] = w[1] ^ k0.y; s[p][2] = w[2] ^ k0.z; s[p][3] = w[3] ^ k0.w;
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round1_macinput<TAB>(s[p], ukey->row(11), l);
-        else round1_macinput<TAB>(s[p], LdsKey(slot[p]).row(11), l);
-    }
-#pragma unroll
-    for (int r = 2; r < 10; ++r) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            if constexpr (KEYSEL == HFV_KEYSEL_ZERO) round_full<TAB>(s[p], ukey->template rk<TAB>(r), l);
-            else round_full<TAB>(s[p], LdsKey(slot[p]).template rk<TAB>(r), l);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        uint32_t t0, t1;
-        bool ok = (t + p * nwaves) * 64 + lane < n;
-        if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-            round_last_48<TAB>(s[p], ukey->row(10), l, t0, t1);
-        } else {
-            const LdsKey key(slot[p]);
-            round_last_48<TAB>(s[p], key.row(10), l, t0, t1);
-            ok = ok && key.ok();
-        }
-        bool pass = ok && rec_tag_matches(cur[p], t0, t1);
-        uint64_t ballot = __ballot(pass);
-        if constexpr (RET)
-            ret[p] = ballot;
-        else if (lane == 0 && t + p * nwaves < (n + 63) / 64)
-            ((GlobalU64 *)(bits))[t + p * nwaves] = ballot;
-    }
-}
-
-// Per-interface keys gathered into VGPRs (GatherKey) with the 4-table LDS layout: an internal
-// key-selection value for the kernels' template argument (the host still says
-// HFV_KEYSEL_IFID; the slot rule is the same, xdp.c:151-157).
-constexpr int kKeyselGather = 2;
-// ... or with three LDS rows per slot and rounds 3..10's keys expanded per packet (SchedKey).
-constexpr int kKeyselSched = 3;
-
-// One tile with the per-lane key rows already issued (GatherKey::issue): the verdict ballot.
-template <int TAB>
-__device__ __forceinline__ uint64_t verify_tile_gather(const RecWords &r, uint64_t t, uint64_t n, uint32_t lane,
-                                                       const Lane &l, const GatherKey &key)
-{
-    uint32_t w[4];
+    uint32_t w[4], t0, t1;
     rec_macinput(r, w);
-    uint32_t t0, t1;
-    cmac48_macinput<TAB>(w, key, l, t0, t1);
-    const bool pass = t * 64 + lane < n && key.ok() && rec_tag_matches(r, t0, t1);
-    return __ballot(pass);
+    bool ok = in;
+    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
+        cmac48_macinput<4>(w, *ukey, l, t0, t1);
+    } else {
+        const uint32_t slot = rec_key_slot(r);
+        cmac48_sched(w, slot, l, t0, t1);
+        ok = ok && slot_valid(slot);
+    }
+    return __ballot(ok && rec_tag_matches(r, t0, t1));
 }
 
-__device__ __forceinline__ uint64_t verify_tile_sched(const RecWords &r, uint64_t t, uint64_t n, uint32_t lane,
-                                                      const Lane &l)
+// The block's prologue: the round tables from T0 in the kernel arguments (one memory hop, the
+// kernarg segment; round 4: 3.0 us from block entry to the fill barrier, against 4.1-4.5 us
+// with a second hop to a table image), and config 3's key rows.  nthr: the threads taking part.
+template <int KEYSEL, class P>
+__device__ __forceinline__ void fill_block(P t0, const DevKeyTable *tab, uint32_t nthr)
 {
-    uint32_t w[4];
-    rec_macinput(r, w);
-    const uint32_t slot = rec_key_slot(r);
-    uint32_t t0, t1;
-    cmac48_sched(w, slot, l, t0, t1);
-    const bool ok = (s_valid[slot >> 5] >> (slot & 31)) & 1u;
-    const bool pass = t * 64 + lane < n && ok && rec_tag_matches(r, t0, t1);
-    return __ballot(pass);
+    if (threadIdx.x < nthr) fill_ttab_karg<4>(t0, threadIdx.x >> 6, nthr >> 6);
+    if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
+        if (threadIdx.x < nthr) fill_keys5(tab, nthr);
+    }
 }
 
-// STAMP = 1 is a diagnostic build: lane 0 of every wave records s_memrealtime (100 MHz,
-// chip-wide) at entry, after the table fill, after each of its first 10 tiles (12 in the
-// static variant) and at exit into stamps[wave * 16 + k]; the dynamic variant also records
-// s_memtime after the fill and at exit (slots 12, 13) for the in-kernel clock.  Nothing
-// else reads the stamps.
-// Dynamic variant: block b owns the contiguous tile range [b*T/G, (b+1)*T/G) and its waves
-// pull tiles from an LDS counter, so waves that the LDS arbiter serves less often simply
-// take fewer tiles instead of finishing last (static assignment left the last ~20 % of the
-// kernel with few waves active: scripts/stamps.py).  A wave claims its next tile before
-// computing the current one, so the next tile's record loads still overlap the rounds.
-template <int KEYSEL, int BLOCK, int TAB, int DMA, int STAMP>
-__device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ tab,
-                                               const uint32_t *__restrict__ ttab_img,
-                                               const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
-                                               uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
-                                               uint64_t *__restrict__ st, const RecArgs &ka)
+// STAMP = 1 is a diagnostic build (hfv_debug_verify_stamped, scripts/stamps.py): lane 0 of
+// every wave records s_memrealtime (100 MHz, chip-wide) at entry, after the table fill, after
+// each of its first 10 tiles and at exit into stamps[wave * 16 + k], and s_memtime after the
+// fill and at exit (slots 12, 13) for the in-kernel clock.  Nothing else reads the stamps.
+//
+// DYN = 1 (the default): block b owns the contiguous tile range [b*T/G, (b+1)*T/G) and its
+// waves pull tiles from an LDS counter, so waves that the LDS arbiter serves less often take
+// fewer tiles instead of finishing last (a static deal left the last ~20 % of the kernel with
+// few waves active: scripts/stamps.py).  A wave claims its next tile before computing the
+// current one, so the next tile's record loads overlap the rounds.
+// DYN = 0: grid-stride tiles (wave w takes w, w + W, ...), for records in registered host
+// memory, where 256 ranges far apart thrash the GPU's translation of 4 KiB host pages
+// (zero-copy 2^20: 1.60 -> 1.27 ms).
+constexpr int kBlock = 1024;
+constexpr uint32_t kWaves = kBlock / 64;
+
+template <int KEYSEL, int DYN, int STAMP = 0>
+__global__ __launch_bounds__(kBlock) void k_verify_records(const DevKeyTable *__restrict__ tab,
+                                                           const uint8_t *__restrict__ recs, uint64_t stride,
+                                                           uint64_t n, uint32_t inf_off, uint32_t hf_off,
+                                                           uint64_t *__restrict__ bits,
+                                                           uint64_t *__restrict__ stamps, const RecArgs ka)
 {
     const uint64_t ntiles = (n + 63) / 64;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t b0 = ntiles * blockIdx.x / gridDim.x, b1 = ntiles * (blockIdx.x + 1) / gridDim.x;
-    const uint32_t count = (uint32_t)(b1 - b0);
     const uint64_t last = n - 1;
-    const uint32_t kWaves = BLOCK / 64;
-    // first tile of each wave is static (wave index); the queue hands out the rest
-    uint32_t t = wave_uniform(threadIdx.x / 64);
-    UniformKey ukey(ka.key0, ka.key0_ok);   // from the kernel arguments: no second memory hop
-    if (threadIdx.x == 0) s_next_tile = kWaves;
-    // The wave's first records and its share of the table pieces are in flight together;
-    // one vmcnt(0) then covers both (the table must be complete before the barrier).
-    // (Waiting at the barrier only for the table, and for the records after it, needs the
-    // record loads pinned ahead of the barrier and the waitcnt pass told that the LDS-DMA
-    // writes are done; every form tried made the compiler drain the prefetch each tile.)
-    RecWords cur;
-    if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 3) {
-        // the first tile's records, then the tables from T0 in the kernel arguments
-        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
-        fill_ttab_karg<TAB>(ka.t0, threadIdx.x >> 6, BLOCK / 64);
-    } else if constexpr (DMA && BLOCK == 1024 && HFV_FILL == 2) {
-        // table pieces first, then the first tile's records: the pieces land (in order) and are
-        // written to LDS while the records are still on their way from HBM
-        TtabRegs<TAB> tr;
-        tr.issue(ttab_img, threadIdx.x >> 6, BLOCK / 64);
-        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
-        tr.commit(threadIdx.x >> 6, BLOCK / 64);
-    } else {
-        cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
-        if constexpr (DMA) {
-            fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            fill_ttab<TAB>();
-        }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = wave_uniform(threadIdx.x / 64);
+    uint64_t *st = STAMP ? stamps + ((uint64_t)blockIdx.x * kWaves + wv) * 16 : nullptr;
+    if constexpr (STAMP) {
+        if (lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
     }
-    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
+    // DYN: this block's tile range; static: the grid-stride walk
+    const uint64_t b0 = DYN ? ntiles * blockIdx.x / gridDim.x : 0;
+    const uint64_t count = DYN ? ntiles * (blockIdx.x + 1) / gridDim.x - b0 : ntiles;
+    const uint64_t stride_t = DYN ? kWaves : (uint64_t)gridDim.x * kWaves;
+    uint64_t t = DYN ? wv : (uint64_t)blockIdx.x * kWaves + wv;   // the wave's first tile (static)
+    UniformKey ukey(ka.key0, ka.key0_ok);   // from the kernel arguments: no second memory hop
+    if (DYN && threadIdx.x == 0) s_next_tile = kWaves;
+    // the wave's first records are in flight while its share of the tables is written
+    RecWords cur = load_rec(recs, stride, (b0 + t) * 64 + lane, last, inf_off, hf_off);
+    fill_block<KEYSEL>(ka.t0, tab, kBlock);
     __syncthreads();
     const Lane l = lane_bases();
-    int nst = 0;
     if constexpr (STAMP) {
         if (lane == 0) {
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[12] = __builtin_amdgcn_s_memtime();   // shader clock, for the in-kernel frequency
         }
     }
-    const UniformKey *ukp = nullptr;
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
         if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
-            for (uint32_t tt = t; tt < count; tt += kWaves)
+            for (uint64_t tt = t; tt < count; tt += stride_t)
                 if (lane == 0) bits[b0 + tt] = 0;
             return;
         }
-        ukp = &ukey;
     }
     // Verdict words wait in a per-wave stash (lane j: the wave's j-th tile) and go out as one
-    // store per 64 tiles: a store per tile sits in the in-order vmcnt queue, and the loop
-    // latch (which waits for the prefetched record words) would wait for its write
-    // acknowledgement every tile.
-    uint64_t st_word = 0;
-    uint32_t st_tile = 0, stashed = 0;
+    // store per 64 tiles: a store per tile sits in the in-order vmcnt queue, and the loop latch
+    // (which waits for the prefetched record words) would wait for its write acknowledgement
+    // every tile.
+    uint64_t st_word = 0, st_tile = 0;
+    uint32_t stashed = 0;
+    int nst = 0;
     while (t < count) {
-        uint32_t nt = 0;
-        if (lane == 0) nt = atomicAdd(&s_next_tile, 1u);
-        nt = wave_uniform(nt);
+        uint64_t nt;
+        if constexpr (DYN) {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(&s_next_tile, 1u);
+            nt = wave_uniform(c);
+        } else {
+            nt = t + stride_t;
+        }
         RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
-        RecWords c1[1] = {cur};
-        uint64_t ballot;
-        verify_tiles<KEYSEL, TAB, 1, 1>(c1, b0 + t, 0, n, lane, l, ukp, nullptr, &ballot);
+        const uint64_t ballot = verify_tile<KEYSEL>(cur, (b0 + t) * 64 + lane < n, l, &ukey);
         if (lane == stashed) {
             st_word = ballot;
-            st_tile = t;
+            st_tile = b0 + t;
         }
         if (++stashed == 64) {
-            ((GlobalU64 *)bits)[b0 + st_tile] = st_word;
+            ((GlobalU64 *)bits)[st_tile] = st_word;
             stashed = 0;
         }
         if constexpr (STAMP) {
@@ -340,339 +213,10 @@ __device__ __forceinline__ void verify_dynamic(const DevKeyTable *__restrict__ t
         cur = nxt;
         t = nt;
     }
-    if (lane < stashed) ((GlobalU64 *)bits)[b0 + st_tile] = st_word;
+    if (lane < stashed) ((GlobalU64 *)bits)[st_tile] = st_word;
     if constexpr (STAMP) {
         if (lane == 0) {
             st[13] = __builtin_amdgcn_s_memtime();
-            st[15] = __builtin_amdgcn_s_memrealtime();
-            st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-                     ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// bitsliced verify (hfv_bitslice.h): VALU-only AES for chunks of 512 records per wave
-// ---------------------------------------------------------------------------------------
-// Per-wave LDS staging of a chunk: 6 words per record (macinput w0..w3, expected MAC words
-// e0 = mac0..3, e1 = mac4..5), quad q's 32 records at dword q * kBsQuadStride + 6 p.  The
-// 4-dword pad per quad makes the transposing reads (lane (q, c) reads word c of record p of
-// quad q, all lanes the same p) bank-conflict free: bank = (4 q + c + 6 p) % 32.
-constexpr uint32_t kBsChunk = 512;                 // records per wave per chunk = 8 tiles
-constexpr uint32_t kBsQuadStride = 32 * 6 + 4;     // dwords
-constexpr uint32_t kBsWaveDwords = 16 * kBsQuadStride;
-constexpr uint32_t kBsMaxWaves = 4;
-static __shared__ uint32_t s_bs[kBsMaxWaves * kBsWaveDwords];   // 49 KiB
-static __shared__ uint32_t s_fill_done;
-
-// AddRoundKey + ShiftRows on the quad: row r of lane c comes from lane (c + r) % 4
-// (DPP quad_perm on the XOR's first operand).
-template <int R>
-__device__ __forceinline__ uint32_t quad_rot(uint32_t v)
-{
-    constexpr int ctrl = R == 1 ? 0x39 : R == 2 ? 0x4e : 0x93;   // quad_perm [1230], [2301], [3012]
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
-}
-__device__ __forceinline__ void bs_ark_sr(uint32_t (&s)[32], uint32_t kk)
-{
-#pragma unroll
-    for (int b = 0; b < 8; ++b) s[b] ^= bs::kmask(kk, b);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) s[8 + b] = quad_rot<1>(s[8 + b]) ^ bs::kmask(kk, 8 + b);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) s[16 + b] = quad_rot<2>(s[16 + b]) ^ bs::kmask(kk, 16 + b);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) s[24 + b] = quad_rot<3>(s[24 + b]) ^ bs::kmask(kk, 24 + b);
-}
-
-// The lane's key column for the ARK+SR step before round r + 1 (r = 0..9): row 0 of the
-// device key image is rk0 ^ K1, rows 1..9 are rot16 of rk1..rk9 (hfv_tables.h).  The row is
-// a wave-uniform scalar load (K$), so the round loop need not be unrolled to keep keys in
-// registers.
-// The four candidate words are formed on the scalar unit; the lane picks its column with
-// per-lane all-ones/all-zeros selectors (sel[k] = -(c == k)), so nothing branches on c.
-struct BsLaneSel {
-    uint32_t sel[4];
-    __device__ __forceinline__ explicit BsLaneSel(uint32_t c)
-    {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sel[k] = vconst(0) - (c == (uint32_t)k ? 1u : 0u);
-    }
-    __device__ __forceinline__ uint32_t pick(const uint32_t (&w)[4]) const
-    {
-        return (w[0] & sel[0]) | (w[1] & sel[1]) | (w[2] & sel[2]) | (w[3] & sel[3]);
-    }
-};
-__device__ __forceinline__ uint32_t bs_round_key(const DevKeyTable *tab, uint32_t r, const BsLaneSel &ls)
-{
-    const uint32_t *p = tab->rows[r][0];
-    uint32_t w[4] = {p[0], p[1], p[2], p[3]};
-    if (r >= 1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = (w[i] >> 16) | (w[i] << 16);
-    }
-    uint32_t k[4];   // k[c] = the pre-shifted key column of lane c (bs::shifted_key_column)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        k[c] = (w[c] & 0xffu) | (w[(c + 1) & 3] & 0xff00u) | (w[(c + 2) & 3] & 0xff0000u) | (w[(c + 3) & 3] & 0xff000000u);
-    return ls.pick(k);
-}
-// column c of rk10, added after the last SubBytes (no shift)
-__device__ __forceinline__ uint32_t bs_final_key(const DevKeyTable *tab, const BsLaneSel &ls)
-{
-    const uint32_t *p = tab->rows[10][0];
-    const uint32_t w[4] = {p[0], p[1], p[2], p[3]};
-    return ls.pick(w);
-}
-
-// One chunk of up to 512 records [base, base + 512) by one wave: coalesced record loads
-// (8 tiles), macinput + expected words staged in the wave's LDS region, transposed into
-// bit planes per quad, 10 bitsliced rounds, then the 48-bit compare (xdp.c:89-90) in the
-// bitsliced domain: lane 0 of a quad holds tag bytes 0..3 (column 0), lane 1 bytes 4..5.
-// Records >= limit get a 0 bit; words32 = number of 32-bit bitmap words that may be written.
-__device__ __forceinline__ void bs_chunk(const uint8_t *__restrict__ recs, uint64_t stride, uint64_t base,
-                                         uint64_t limit, uint32_t inf_off, uint32_t hf_off, uint32_t *lds,
-                                         const DevKeyTable *__restrict__ tab, uint32_t *__restrict__ bits32, uint64_t words32,
-                                         uint32_t lane)
-{
-    const uint64_t last = limit - 1;
-    RecWords r[8];
-#pragma unroll
-    for (int it = 0; it < 8; ++it) r[it] = load_rec(recs, stride, base + it * 64 + lane, last, inf_off, hf_off);
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        uint32_t w[4];
-        rec_macinput(r[it], w);
-        uint32_t e0 = __builtin_amdgcn_alignbit(r[it].hfb, r[it].hfa.y, 16), e1 = r[it].hfb >> 16;
-        uint32_t *d = lds + (2 * it + (lane >> 5)) * kBsQuadStride + 6 * (lane & 31);
-        *reinterpret_cast<uint2 *>(d) = make_uint2(w[0], w[1]);
-        *reinterpret_cast<uint2 *>(d + 2) = make_uint2(w[2], w[3]);
-        *reinterpret_cast<uint2 *>(d + 4) = make_uint2(e0, e1);
-    }
-    const uint32_t q = lane >> 2, c = lane & 3;
-    const BsLaneSel ls(c);
-    const uint32_t *src = lds + q * kBsQuadStride + c;
-    uint32_t s[32];
-#pragma unroll
-    for (int p = 0; p < 32; ++p) s[p] = src[6 * p];
-    bs::transpose32(s);
-#pragma unroll 1
-    for (uint32_t rd = 0; rd < 9; ++rd) {
-        bs_ark_sr(s, bs_round_key(tab, rd, ls));
-        bs::sub_bytes(s);
-        bs::mix_columns(s);
-    }
-    bs_ark_sr(s, bs_round_key(tab, 9, ls));
-    bs::sub_bytes(s);
-    const uint32_t k10 = bs_final_key(tab, ls);
-    uint32_t e[32];
-    const uint32_t *es = lds + q * kBsQuadStride + 4 + (c & 1);
-#pragma unroll
-    for (int p = 0; p < 32; ++p) e[p] = es[6 * p];
-    bs::transpose32(e);
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) lo |= HFV_BOP3(s[i], e[i], bs::kmask(k10, i), 0x96);
-#pragma unroll
-    for (int i = 16; i < 32; ++i) hi |= HFV_BOP3(s[i], e[i], bs::kmask(k10, i), 0x96);
-    uint32_t m = lo | (c == 0 ? hi : 0u);
-    m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x55, 0xf, 0xf, false);   // quad_perm [1111]: + lane 1
-    const uint64_t first = base + 32 * q;
-    uint32_t valid = first >= limit ? 0u : (limit - first >= 32 ? ~0u : ((1u << (limit - first)) - 1u));
-    const uint64_t word = base / 32 + q;
-    if (c == 0 && word < words32) bits32[word] = ~m & valid;
-}
-
-// Pure bitsliced verify (KEYSEL_ZERO): every wave works through 512-record chunks.
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_verify_bs(const DevKeyTable *__restrict__ tab,
-                                                     const uint32_t *__restrict__ ttab_img,
-                                                     const uint8_t *__restrict__ recs, uint64_t stride, uint64_t n,
-                                                     uint32_t inf_off, uint32_t hf_off, uint64_t *__restrict__ bits,
-                                                     uint64_t *__restrict__ stamps, const RecArgs ka)
-{
-    static_assert(BLOCK / 64 <= (int)kBsMaxWaves, "LDS staging regions");
-    const uint32_t lane = threadIdx.x & 63, wv = wave_uniform(threadIdx.x / 64);
-    const uint64_t nchunks = (n + kBsChunk - 1) / kBsChunk, words32 = 2 * ((n + 63) / 64);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
-    UniformKey ukey(tab);
-    uint32_t *bits32 = reinterpret_cast<uint32_t *>(bits);
-    if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
-        for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < words32; w += (uint64_t)gridDim.x * BLOCK)
-            bits32[w] = 0;
-        return;
-    }
-    uint32_t *lds = s_bs + wv * kBsWaveDwords;
-    for (uint64_t ch = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; ch < nchunks; ch += nwaves)
-        bs_chunk(recs, stride, ch * kBsChunk, n, inf_off, hf_off, lds, tab, bits32, words32, lane);
-}
-
-// Hybrid verify (KEYSEL_ZERO): per block, NBS waves run the bitsliced VALU path on 512-record
-// chunks while the other waves run the LDS T-table path on 64-record tiles, both pulling
-// from the block's tile queue over its contiguous tile range.  Only the T-table waves wait
-// for the table fill (an LDS counter, not a block barrier), so the bitsliced waves start at
-// once.  A bitsliced wave stops claiming when fewer than kBsStop tiles would remain for the
-// T-table waves, so the block does not end on a long bitsliced chunk.
-template <int BLOCK, int NBS>
-__global__ __launch_bounds__(BLOCK) void k_verify_hybrid(const DevKeyTable *__restrict__ tab,
-                                                         const uint32_t *__restrict__ ttab_img,
-                                                         const uint8_t *__restrict__ recs, uint64_t stride,
-                                                         uint64_t n, uint32_t inf_off, uint32_t hf_off,
-                                                         uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps,
-                                                         const RecArgs ka)
-{
-    static_assert(NBS >= 1 && NBS <= (int)kBsMaxWaves && NBS < BLOCK / 64, "wave roles");
-    constexpr uint32_t kWaves = BLOCK / 64, kTT = kWaves - NBS;
-    constexpr uint32_t kChunkTiles = kBsChunk / 64;
-    constexpr uint32_t kBsStop = kChunkTiles + 2 * kTT;
-    const uint64_t ntiles = (n + 63) / 64;
-    const uint32_t lane = threadIdx.x & 63, wv = wave_uniform(threadIdx.x / 64);
-    const uint64_t b0 = ntiles * blockIdx.x / gridDim.x, b1 = ntiles * (blockIdx.x + 1) / gridDim.x;
-    const uint32_t count = (uint32_t)(b1 - b0);
-    const uint64_t last = n - 1;
-    UniformKey ukey(tab);
-    RecWords cur = load_rec(recs, stride, (b0 + (wv < kTT ? wv : 0)) * 64 + lane, last, inf_off, hf_off);
-    if (threadIdx.x == 0) {
-        s_next_tile = kTT;   // tiles 0..kTT-1 are the T-table waves' first tiles
-        s_fill_done = 0;
-    }
-    __syncthreads();
-    if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
-        for (uint32_t t = wv; t < count; t += kWaves)
-            if (lane == 0) bits[b0 + t] = 0;
-        return;
-    }
-    if (wv >= kTT) {   // bitsliced waves
-        uint32_t *lds = s_bs + (wv - kTT) * kBsWaveDwords;
-        uint32_t *bits32 = reinterpret_cast<uint32_t *>(bits);
-        for (;;) {
-            uint32_t t0 = count;
-            if (lane == 0) {
-                uint32_t head = __hip_atomic_load(&s_next_tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (head + kBsStop <= count) t0 = atomicAdd(&s_next_tile, kChunkTiles);
-            }
-            t0 = wave_uniform(t0);
-            if (t0 >= count) break;
-            const uint32_t t1 = t0 + kChunkTiles < count ? t0 + kChunkTiles : count;
-            const uint64_t lim = (b0 + t1) * 64 < n ? (b0 + t1) * 64 : n;
-            bs_chunk(recs, stride, (b0 + t0) * 64, lim, inf_off, hf_off, lds, tab, bits32, 2 * (b0 + t1), lane);
-        }
-        return;
-    }
-    // T-table waves: share the table fill, then wait on the LDS counter (acquire) for all of it
-    {
-        const int nw = kTT;
-        char *ldst = reinterpret_cast<char *>(s_tab64);
-        for (int ch = wv; ch < 64; ch += nw) {
-            const char *src = ttab_src(ttab_img, ch, lane);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)(ldst + ch * 1024), 16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(&s_fill_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__hip_atomic_load(&s_fill_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kTT)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_s_setprio(3);   // issue ahead of the bitsliced waves on a shared SIMD
-    const Lane l = lane_bases();
-    uint32_t t = wv;
-    while (t < count) {
-        uint32_t nt = 0;
-        if (lane == 0) nt = atomicAdd(&s_next_tile, 1u);
-        nt = wave_uniform(nt);
-        RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
-        RecWords c1[1] = {cur};
-        verify_tiles<HFV_KEYSEL_ZERO, 2, 1>(c1, b0 + t, 0, n, lane, l, &ukey, bits);
-        cur = nxt;
-        t = nt;
-    }
-}
-
-template <int KEYSEL, int BLOCK, int PF, int TAB, int DMA, int NP, int STAMP = 0, int DYN = 0>
-__global__ __launch_bounds__(BLOCK) void k_verify_records(const DevKeyTable *__restrict__ tab,
-                                                          const uint32_t *__restrict__ ttab_img,
-                                                          const uint8_t *__restrict__ recs, uint64_t stride,
-                                                          uint64_t n, uint32_t inf_off, uint32_t hf_off,
-                                                          uint64_t *__restrict__ bits, uint64_t *__restrict__ stamps,
-                                                          const RecArgs ka)
-{
-    static_assert(PF == 1 || PF == 2, "prefetch depth");
-    static_assert(NP == 1 || NP == 2, "packets per lane");
-    static_assert(KEYSEL == HFV_KEYSEL_ZERO || TAB == 2, "per-lane keys need the 64 KiB table layout");
-    constexpr uint32_t kWaves = BLOCK / 64;
-    const uint64_t ntiles = (n + 63) / 64;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = wave_uniform(blockIdx.x * kWaves + threadIdx.x / 64);
-    const uint64_t nwaves = gridDim.x * kWaves;
-    uint64_t *st = STAMP ? stamps + (uint64_t)wave * 16 : nullptr;
-    int nst = 0;
-    if constexpr (STAMP) {
-        if (lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
-    }
-
-    if constexpr (DYN) {
-        verify_dynamic<KEYSEL, BLOCK, TAB, DMA, STAMP>(tab, ttab_img, recs, stride, n, inf_off, hf_off, bits, st, ka);
-        return;
-    }
-    // First tiles' record loads go out before the table fill so the fill overlaps their
-    // memory latency.
-    const uint64_t last = n - 1;
-    const uint64_t step = NP * nwaves;   // tiles consumed per iteration by the whole grid
-    uint64_t t = wave;
-    RecWords cur[NP], nx1[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) cur[p] = load_rec(recs, stride, (t + p * nwaves) * 64 + lane, last, inf_off, hf_off);
-    if constexpr (PF == 2) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-            nx1[p] = load_rec(recs, stride, (t + step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
-    }
-    UniformKey ukey(tab);
-
-    if constexpr (DMA) {
-        fill_ttab_dma_issue<TAB, BLOCK>(ttab_img);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-        fill_ttab<TAB>();
-    }
-    if constexpr (KEYSEL == HFV_KEYSEL_IFID) fill_keys(tab);
-    __syncthreads();
-    const Lane l = lane_bases();
-    if constexpr (STAMP) {
-        if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-    }
-
-    const UniformKey *ukp = nullptr;
-    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        if (!ukey.ok) {   // no key in slot 0: every packet fails closed (xdp.c:83-84)
-            for (uint64_t tt = wave; tt < ntiles; tt += nwaves)
-                if (lane == 0) bits[tt] = 0;
-            return;
-        }
-        ukp = &ukey;
-    }
-    for (; t < ntiles; t += step) {
-        RecWords nxt[NP];
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-            nxt[p] = load_rec(recs, stride, (t + PF * step + p * nwaves) * 64 + lane, last, inf_off, hf_off);
-        verify_tiles<KEYSEL, TAB, NP>(cur, t, nwaves, n, lane, l, ukp, bits);
-        if constexpr (STAMP) {
-            if (lane == 0 && nst < 12) st[2 + nst] = __builtin_amdgcn_s_memrealtime();
-            ++nst;
-        }
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            if constexpr (PF == 2) {
-                cur[p] = nx1[p];
-                nx1[p] = nxt[p];
-            } else {
-                cur[p] = nxt[p];
-            }
-        }
-    }
-    if constexpr (STAMP) {
-        if (lane == 0) {
             st[15] = __builtin_amdgcn_s_memrealtime();
             // placement: HW_REG_HW_ID (hwreg 4, all 32 bits) and HW_REG_XCC_ID (hwreg 20)
             st[14] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
@@ -730,11 +274,23 @@ __device__ __forceinline__ uint64_t karg_cum(KArgs a, uint64_t k)
     return svc_cum(w, k);
 }
 
+// Experiment switches (A/B builds only, scripts/mkvar_k.sh; the defaults are the product):
+// HFV_SVC_NP = 2: a claim takes two consecutive tiles of the block's share, verified together
+// (two independent AES chains per wave); HFV_SVC_NT = 1: non-temporal record loads.
+#ifndef HFV_SVC_NP
+#define HFV_SVC_NP 1
+#endif
+#ifndef HFV_SVC_NT
+#define HFV_SVC_NT 0
+#endif
+constexpr uint32_t kSvcNP = HFV_SVC_NP;
+static_assert(kSvcNP == 1 || kSvcNP == 2, "tiles per claim");
+
 struct alignas(16) SvcSlot {
-    uint32_t base, count;   // block tile numbers [base, base + count)
-    uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
+    uint32_t base, count;   // block claim numbers [base, base + count); a claim is kSvcNP tiles
+    uint32_t done, stop;    // claims of the batch this block has verified; 1: exit descriptor
     uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the block's range
-    uint64_t pad;
+    uint64_t ntiles;        // tiles of the block's range
 };
 static __shared__ SvcSlot s_svc[kSvcRing];
 static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
@@ -750,9 +306,9 @@ __device__ __forceinline__ void svc_share(uint64_t ntiles, uint64_t &t0, uint32_
     count = (uint32_t)(ntiles * s_svc_c1 / s_svc_w - t0);
 }
 
-struct SvcTile {   // one claimed tile, wave-uniform
-    uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + (g - base)
-    uint32_t b, base, count;
+struct SvcTile {   // one claim, wave-uniform
+    uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + kSvcNP * (g - base): its first tile
+    uint32_t b, base, count, ntiles;
 };
 enum SvcClaim { kSvcFound = 0, kSvcStop = 1, kSvcPending = 2 };
 
@@ -769,76 +325,35 @@ __device__ __forceinline__ RecWords load_tile(const SvcTile &t, uint32_t lane, u
     typedef const __attribute__((address_space(1))) u32x2 *P2;
     typedef const __attribute__((address_space(1))) uint32_t *P1;
     RecWords r;
-    const u32x2 a = *reinterpret_cast<P2>(p + inf_off);
-    const u32x2 b = *reinterpret_cast<P2>(p + hf_off);
-    r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
+    u32x2 a, b;
+    if constexpr (HFV_SVC_NT) {
+        a = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
+        b = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
+        r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
+    } else {
+        a = *reinterpret_cast<P2>(p + inf_off);
+        b = *reinterpret_cast<P2>(p + hf_off);
+        r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
+    }
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
     return r;
+}
+
+// The claim's second tile (kSvcNP = 2), or its first again when the block's range has an odd
+// tile count and this is its last claim.
+__device__ __forceinline__ SvcTile second_tile(const SvcTile &t, bool &valid)
+{
+    SvcTile u = t;
+    valid = t.tile - t.tile0 + 1 < t.ntiles;
+    u.tile += valid ? 1 : 0;
+    return u;
 }
 
 __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 {
     return (uint64_t)wave_uniform((uint32_t)x) | ((uint64_t)wave_uniform((uint32_t)(x >> 32)) << 32);
 }
-
-#ifndef HFV_SVC_ACQ
-#define HFV_SVC_ACQ 1   // 0: none, 1: acquire fence per loaded batch, 2: system-scope record loads
-#endif
-// HFV_SVC_PROF = 1: diagnostic build; every wave sums the shader cycles (s_memtime) it spends
-// in each phase of the service loop and adds them to host->prof[] at exit:
-//   0 waiting for the current tile's records at the top of the loop, 1 claim + map + next
-//   tile's loads, 2 the tile's AES rounds and verdict, 3 verdict stores + completion count,
-//   4 blocking waits for a descriptor, 5 tiles verified, 6 the wave's whole loop.
-#ifndef HFV_SVC_PROF
-#define HFV_SVC_PROF 0
-#endif
-// HFV_SVC_SPAN = 1: diagnostic build; block entry, table-fill and wave exit stamps
-// (s_memrealtime, 100 MHz) into dev->span_* (hfv_debug_service_span)
-#ifndef HFV_SVC_SPAN
-#define HFV_SVC_SPAN 0
-#endif
-// HFV_SVC_AHEAD = 1: the next tile's number is claimed one iteration early (a wave then holds
-// three tiles: the one it computes, the one whose records are loading, the claimed one); 0 (the
-// default): it is claimed at the top of the iteration that loads its records, so a wave holds
-// two and the block's last tiles go to whichever waves are free one tile-time later: K = 20
-// grids 2.1-2.4 % shorter (profiles/r03/ahead_ab/), the claim's LDS latency is not missed.
-#ifndef HFV_SVC_AHEAD
-#define HFV_SVC_AHEAD 0
-#endif
-// Only wave 1 of every block samples (s_memtime from every wave of a CU slowed the loop
-// many times over); the other waves run the plain loop beside it.
-struct SvcProf {
-    uint64_t c[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint64_t t = 0;
-    bool on = false;
-    __device__ __forceinline__ void start()
-    {
-        if constexpr (HFV_SVC_PROF) {
-            on = wave_uniform(threadIdx.x >> 6) == 1;
-            if (on) t = __builtin_amdgcn_s_memtime();
-        }
-    }
-    __device__ __forceinline__ void mark(int k)
-    {
-        if constexpr (HFV_SVC_PROF) {
-            if (!on) return;
-            uint64_t now = __builtin_amdgcn_s_memtime();
-            c[k] += now - t;
-            t = now;
-        }
-    }
-    __device__ __forceinline__ void flush(SvcShared *host, uint32_t lane, uint64_t t0)
-    {
-        if constexpr (HFV_SVC_PROF) {
-            if (!on) return;
-            c[6] = __builtin_amdgcn_s_memtime() - t0;
-            if (lane == 0)
-                for (int k = 0; k < 7; ++k)
-                    __hip_atomic_fetch_add(&host->prof[k], c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-};
 
 // This block's share of batch b is verified (one lane).  The verdict words were written
 // through to memory (system-scope stores) and every wave waited for their acknowledgement
@@ -1021,13 +536,9 @@ __device__ __attribute__((noinline)) bool svc_load(KArgs a, uint32_t b, bool blo
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // fields only after seq was seen
-#if HFV_SVC_ACQ == 1
     // the batch's records were written (by a kernel or a copy into device memory) before the
     // host posted it: drop this CU's stale L1 lines (agent scope, buffer_inv sc1)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#elif HFV_SVC_ACQ == 3
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope (buffer_inv sc0 sc1: L1 and L2)
-#endif
     if (blockIdx.x == 0) dev->load_clock[slot] = memrealtime();
     SvcSlot &s = s_svc[slot];
     const SvcSlot &p = s_svc[(b + kSvcRing - 1) % kSvcRing];
@@ -1050,7 +561,8 @@ __device__ __attribute__((noinline)) bool svc_load(KArgs a, uint32_t b, bool blo
         svc_share((n + 63) / 64, t0, cnt);
         s.n = n;
         s.tile0 = t0;
-        s.count = cnt;
+        s.ntiles = cnt;
+        s.count = (cnt + kSvcNP - 1) / kSvcNP;
         if (s.count == 0) svc_complete(dev, a->tag, b);
     }
     __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1079,7 +591,8 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
             cnt = (uint32_t)(nt * c1 / w - t0);
         }
     }
-    uint32_t incl = cnt;   // inclusive prefix sum of the counts over the lanes
+    const uint32_t units = (cnt + kSvcNP - 1) / kSvcNP;   // claims
+    uint32_t incl = units;   // inclusive prefix sum of the claim counts over the lanes
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
@@ -1087,8 +600,9 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
     }
     if (lane < n_in) {
         SvcSlot &s = s_svc[lane];
-        s.base = incl - cnt;
-        s.count = cnt;
+        s.base = incl - units;
+        s.count = units;
+        s.ntiles = cnt;
         s.done = 0;
         s.stop = stop;
         s.recs = d.recs;
@@ -1124,7 +638,7 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
 {
     if (g - hint.base < hint.count) {   // same batch as the wave's current tile: no LDS reads
         t = hint;
-        t.tile = hint.tile0 + (g - hint.base);
+        t.tile = hint.tile0 + kSvcNP * (g - hint.base);
         return kSvcFound;
     }
     uint64_t t_wait = 0;
@@ -1154,7 +668,8 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
             t.n = wave_uniform64(s.n);
             t.stride = wave_uniform64(s.stride);
             t.tile0 = wave_uniform64(s.tile0);
-            t.tile = t.tile0 + (g - base);
+            t.tile = t.tile0 + kSvcNP * (g - base);
+            t.ntiles = wave_uniform((uint32_t)s.ntiles);
             t.b = b;
             t.base = base;
             t.count = count;
@@ -1190,8 +705,8 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
     }
 }
 
-template <int KEYSEL, int TAB>
-__global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
+template <int KEYSEL>
+__global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
 {
     // the fields through the kernarg segment pointer (constant address space): no private copy
     // of the 2.4 KB argument struct, and helpers take the pointer
@@ -1199,7 +714,6 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     (void)args;
     const uint32_t lane = threadIdx.x & 63;
     SvcDev *dev = a->dev;
-    if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_entry[blockIdx.x] = memrealtime();
     UniformKey ukey(a->key0, a->key0_ok);
     const uint32_t inf_off = a->inf_off, hf_off = a->hf_off;
     if (threadIdx.x == 0) {
@@ -1218,25 +732,12 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     // starts relaying right after it.
     const uint32_t nthr = blockIdx.x == 0 ? 1024 - 64 : 1024;   // threads filling the tables
     const bool relay = blockIdx.x == 0 && threadIdx.x >= nthr;
-#if HFV_SVC_FILL_DMA
-    if (!relay) fill_ttab_dma_issue_n<TAB>(a->ttab_img, threadIdx.x >> 6, nthr >> 6);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-    if (!relay) fill_ttab_karg<TAB>(a->t0, threadIdx.x >> 6, nthr >> 6);
-#endif
-    if constexpr (KEYSEL == HFV_KEYSEL_IFID) {
-        if (!relay) fill_keys(a->tab, nthr);
-    } else if constexpr (KEYSEL == kKeyselGather) {
-        fill_valid(a->tab);
-    } else if constexpr (KEYSEL == kKeyselSched) {
-        if (!relay) fill_keys3(a->tab, nthr);
-    }
+    fill_block<KEYSEL>(a->t0, a->tab, nthr);
     __syncthreads();
     if (threadIdx.x == 0) {
         dev->blk_start[blockIdx.x] = memrealtime();
         dev->blk_clk0[blockIdx.x] = __builtin_amdgcn_s_memtime();
     }
-    if (HFV_SVC_SPAN && threadIdx.x == 0) dev->span_fill[blockIdx.x] = memrealtime();
     if (relay) {   // no barrier follows: the block's other waves go on without it
         svc_relay(a, lane, gridDim.x);
         return;
@@ -1255,13 +756,14 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     none.base = 0;
     none.count = 0;
     // The loop, per tile: wait for the tile's records (loaded one iteration ahead), claim the
-    // next tile (LDS atomic; HFV_SVC_AHEAD = 1 claimed it one iteration earlier still), store the
+    // next tile (LDS atomic, just in time: claiming one iteration ahead made K = 20 grids 2.1-2.4 %
+    // longer, profiles/ab_index.md r03_ahead_ab), store the
     // verdict words of a batch the wave left in the previous
     // iteration (so their write acknowledgement arrives while this tile computes and is
     // covered by the next iteration's wait), map the next tile and issue its loads, compute.
-    // Measured with the HFV_SVC_PROF build on the loop this replaces (claim at the top, store
-    // and a vmcnt(0) drain when leaving a batch): claim/map/load 10 %, store/count drain
-    // 9-20 % of a wave's cycles.
+    // (Measured with a phase-counter build on the loop this replaces -- claim at the top, store
+    // and a vmcnt(0) drain when leaving a batch: claim/map/load 10 %, store/count drain 9-20 %
+    // of a wave's cycles.)
     auto claim = [&]() -> uint32_t {
         uint32_t g = 0;
         if (lane == 0) g = __hip_atomic_fetch_add(&s_svc_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1269,7 +771,6 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
     };
     SvcTile cur;
     if (svc_map(a, lane, wave_uniform(claim()), true, mb, none, cur) != kSvcFound) return;
-    uint32_t gq = HFV_SVC_AHEAD ? claim() : 0u;   // the next tile's number (lane 0), read one iteration later
     // Verdict words of cur.b's tiles wait in a per-wave stash (lane j: the j-th word) and go
     // out as ONE scattered write-through store, issued at the top of the iteration after the
     // wave left the batch (or filled the stash).  A store per tile would sit in the wave's
@@ -1294,11 +795,10 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
                                __HIP_MEMORY_SCOPE_SYSTEM);
         stashed = 0;
     };
-    RecWords rc = load_tile(cur, lane, inf_off, hf_off);
+    bool v2 = false;   // kSvcNP = 2: the current claim's second tile exists
+    RecWords rc = load_tile(cur, lane, inf_off, hf_off), rc2 = rc;
+    if constexpr (kSvcNP == 2) rc2 = load_tile(second_tile(cur, v2), lane, inf_off, hf_off);
     svc_prefetch(a, lane, cur.b);
-    SvcProf prof;
-    const uint64_t prof_t0 = HFV_SVC_PROF ? __builtin_amdgcn_s_memtime() : 0;
-    prof.start();
     for (;;) {
         // This tile's record words (and every earlier store) are complete.  An explicit wait
         // (a builtin, so the waitcnt pass sees it): without it the pass merges the loop's
@@ -1306,7 +806,6 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
         count(dc_b, dc_count, dc_k);           // the stores of the previous iteration are acknowledged
         dc_k = 0;
-        prof.mark(0);
         if (flush) {                           // the batch left in the previous iteration
             store_stash();
             dc_b = fl_b;
@@ -1314,39 +813,30 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
             dc_k = fl_k;
             flush = false;
         }
-        // per-interface keys: this tile's key rows, issued BEFORE the next tile's record loads
-        // (vmcnt retires in order: a row wait must not also wait for those HBM loads)
-        GatherKey gk;
-        if constexpr (KEYSEL == kKeyselGather) gk.issue(a->tab, rec_key_slot(rc));
-        uint32_t g;
-        if constexpr (HFV_SVC_AHEAD) {
-            g = wave_uniform(gq);
-            gq = claim();
-        } else {
-            g = wave_uniform(claim());
-        }
+        const uint32_t g = wave_uniform(claim());
         SvcTile nx;
         SvcClaim c = svc_map(a, lane, g, false, mb, cur, nx);
         if (c != kSvcFound) nx = cur;
-        RecWords rn = load_tile(nx, lane, inf_off, hf_off);
-        prof.mark(1);
-        uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
-        if constexpr (KEYSEL == kKeyselGather) {
-            ballot = verify_tile_gather<TAB>(rc, cur.tile, cur.n, lane, l, gk);
-        } else if constexpr (KEYSEL == kKeyselSched) {
-            ballot = verify_tile_sched(rc, cur.tile, cur.n, lane, l);
-        } else if (keyok) {
-            RecWords c1[1] = {rc};
-            verify_tiles<KEYSEL, TAB, 1, 1>(c1, cur.tile, 0, cur.n, lane, l, ukp, nullptr, &ballot);
+        bool nv2 = false;
+        RecWords rn = load_tile(nx, lane, inf_off, hf_off), rn2 = rn;
+        if constexpr (kSvcNP == 2) rn2 = load_tile(second_tile(nx, nv2), lane, inf_off, hf_off);
+        uint64_t ballot = 0, ballot2 = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
+        if (keyok) {
+            ballot = verify_tile<KEYSEL>(rc, cur.tile * 64 + lane < cur.n, l, ukp);
+            if constexpr (kSvcNP == 2) ballot2 = verify_tile<KEYSEL>(rc2, (cur.tile + 1) * 64 + lane < cur.n, l, ukp);
         }
-        if constexpr (HFV_SVC_PROF) prof.c[5] += 1;
-        prof.mark(2);
         if (lane == stashed) {
             st_word = ballot;
             st_tile = cur.tile;
         }
+        if constexpr (kSvcNP == 2) {   // the second tile's word, or the first's again (same address)
+            if (lane == stashed + 1) {
+                st_word = v2 ? ballot2 : ballot;
+                st_tile = cur.tile + (v2 ? 1 : 0);
+            }
+        }
         st_bits = cur.bits;
-        ++stashed;
+        stashed += kSvcNP;
         ++pending;
         const bool leave = c != kSvcFound || nx.b != cur.b;
         if (leave || stashed == 64) {
@@ -1356,7 +846,6 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
             fl_k = leave ? pending : 0;
             if (leave) pending = 0;
         }
-        prof.mark(3);
         if (c != kSvcFound) {
             // before waiting for the host (or leaving): store and count everything verified,
             // so a host that waits for those batches before posting the next never waits on us
@@ -1371,17 +860,19 @@ __global__ __launch_bounds__(1024) void k_verify_service(const SvcArgs args)
             }
             if (c == kSvcPending) {
                 c = svc_map(a, lane, g, true, mb, none, nx);
-                if (c == kSvcFound) rn = load_tile(nx, lane, inf_off, hf_off);
+                if (c == kSvcFound) {
+                    rn = load_tile(nx, lane, inf_off, hf_off);
+                    if constexpr (kSvcNP == 2) rn2 = load_tile(second_tile(nx, nv2), lane, inf_off, hf_off);
+                }
             }
         }
-        prof.mark(4);
         if (c == kSvcStop) break;
         if (nx.b != cur.b) svc_prefetch(a, lane, nx.b);
         cur = nx;
         rc = rn;
+        rc2 = rn2;
+        v2 = nv2;
     }
-    prof.flush(a->host, lane, prof_t0);
-    if (HFV_SVC_SPAN && lane == 0) dev->span_exit[blockIdx.x * 16 + (threadIdx.x >> 6)] = memrealtime();
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dev->run_clock[2] = __builtin_amdgcn_s_memtime();
         dev->run_clock[3] = memrealtime();
@@ -1406,24 +897,11 @@ int launch_debug_spin(void *stream, uint32_t us)
 int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid_out)
 {
-    // Per-interface keys (config 3).  Default: three LDS rows per slot beside all four round
-    // tables, rounds 3..10's keys expanded per packet (SchedKey): bank-conflict cycles 1.37 M ->
-    // 0.38 M per 2^20 batch, LDS-active cycles -6 %, 0.5-2.6 % faster (profiles/r03/pmc/,
-    // ifid_ab/).  HFV_SVC_IFID=lds: the round-2 layout (48 KiB key image beside two tables and
-    // a 16-bit rotation per column).  HFV_SVC_IFID=gather: each packet's key rows gathered from
-    // L2 into VGPRs beside all four tables -- 2x slower (31 vs 63 Gpkt/s, profiles/r03/ifid_gather/):
-    // 11 scattered 16-byte loads per lane per tile hold the vector-memory path ~100 cycles each.
-    static const char *iv = getenv("HFV_SVC_IFID");
-    static const int ifv = !iv ? 2 : !strcmp(iv, "gather") ? 1 : !strcmp(iv, "lds") ? 0 : 2;
-    auto k = keysel != HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_ZERO, 4>
-             : ifv == 1               ? k_verify_service<kKeyselGather, 4>
-             : ifv == 2               ? k_verify_service<kKeyselSched, 4>
-                                      : k_verify_service<HFV_KEYSEL_IFID, 2>;
-    const char *ge = getenv("HFV_SVC_GRID");   // experiments only: fewer blocks than CUs
-    unsigned grid = ge && atoi(ge) > 0 && atoi(ge) < g.num_cus ? (unsigned)atoi(ge) : (unsigned)g.num_cus;
+    auto k = keysel == HFV_KEYSEL_IFID ? k_verify_service<HFV_KEYSEL_IFID> : k_verify_service<HFV_KEYSEL_ZERO>;
+    unsigned grid = g.svc_blocks > 0 && g.svc_blocks < g.num_cus ? (unsigned)g.svc_blocks : (unsigned)g.num_cus;
     if (grid > kSvcMaxBlocks) grid = kSvcMaxBlocks;
     *grid_out = grid;
-    hipExtLaunchKernelGGL(k, dim3(grid), dim3(1024), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, args);
     return (int)hipGetLastError();
 }
@@ -1549,14 +1027,8 @@ __global__ __launch_bounds__(256) void k_expand_keys(const uint4 *__restrict__ r
         p[1] = w[5] ^ tg(2, k0[3] >> 16);
         p[2] = w[6] ^ tg(0, k0[2]);
         p[3] = w[7] ^ tg(1, k0[0] >> 8);
-        uint32_t(*g)[4] = tab->gather[slot];   // slot-major copy (hfv_internal.h)
-        for (int c = 0; c < 4; ++c) {
-            g[0][c] = k0[c];
-            g[1][c] = p[c];
-            g[10][c] = w[40 + c];
-        }
-        for (int r = 2; r < 10; ++r)
-            for (int c = 0; c < 4; ++c) g[r][c] = w[4 * r + c];
+        for (int r = 3; r <= 10; ++r)   // schedule words t_r = w[4r] ^ w[4r-4] (hfv_internal.h)
+            tab->sched[(r - 3) >> 2][slot][(r - 3) & 3] = w[4 * r] ^ w[4 * r - 4];
         atomicOr(&tab->valid[slot >> 5], 1u << (slot & 31));
     }
 }
@@ -1625,9 +1097,6 @@ static inline unsigned grid_for(uint64_t n, int block, int num_cus, int per_cu)
     return (unsigned)(blocks ? blocks : 1);
 }
 
-using VerifyKernel = void (*)(const DevKeyTable *, const uint32_t *, const uint8_t *, uint64_t, uint64_t, uint32_t,
-                              uint32_t, uint64_t *, uint64_t *, const RecArgs);
-
 static RecArgs rec_args(const DevKeyTable *host_keys)
 {
     RecArgs ka;
@@ -1640,66 +1109,30 @@ static RecArgs rec_args(const DevKeyTable *host_keys)
     return ka;
 }
 
-// Record-verify variants (tuning knobs; the default is chosen by scripts/sweep.py data).
-template <int KEYSEL>
-static VerifyKernel pick_verify(const KernelVariant &v)
-{
-    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {   // bitsliced paths: one key for all lanes
-        if (v.bs == kBsOnly) return v.block == 256 ? k_verify_bs<256> : nullptr;
-        if (v.bs > 0) {
-            if (v.block != 1024 || !v.dma || v.tab != 2 || v.np != 1) return nullptr;
-            if (v.bs == 1) return k_verify_hybrid<1024, 1>;
-            if (v.bs == 2) return k_verify_hybrid<1024, 2>;
-            if (v.bs == 3) return k_verify_hybrid<1024, 3>;
-            if (v.bs == 4) return k_verify_hybrid<1024, 4>;
-            return nullptr;
-        }
-    } else {
-        if (v.bs) return nullptr;
-    }
-#define HFV_V(B, P, T)                                                                          \
-    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1 && v.dyn)                        \
-        return k_verify_records<KEYSEL, B, P, T, 1, 1, 0, 1>;                                           \
-    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 1, 1>; \
-    if (v.block == B && v.pf == P && v.tab == T && v.dma && v.np == 2) return k_verify_records<KEYSEL, B, P, T, 1, 2>; \
-    if (v.block == B && v.pf == P && v.tab == T && !v.dma && v.np == 1) return k_verify_records<KEYSEL, B, P, T, 0, 1>;
-    HFV_V(1024, 1, 2) HFV_V(1024, 2, 2) HFV_V(768, 1, 2) HFV_V(512, 1, 2)
-    if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        HFV_V(1024, 1, 4) HFV_V(768, 1, 4)
-    }
-#undef HFV_V
-    return nullptr;
-}
-
 int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, int keysel,
                           const uint8_t *recs,
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream,
                           void *ev_start, void *ev_stop, bool interleaved)
 {
-    KernelVariant v = keysel == HFV_KEYSEL_IFID ? g.multi : g.single;
-    if (interleaved && v.bs == 0) v.dyn = 0;   // the static kernel walks the tiles grid-stride
-    VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(v) : pick_verify<HFV_KEYSEL_ZERO>(v);
-    if (!k) return (int)hipErrorInvalidConfiguration;
-    unsigned grid = grid_for(n, v.block, g.num_cus, v.blocks_per_cu);
-    hipExtLaunchKernelGGL(k, dim3(grid), dim3(v.block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)stride,
-                          (uint64_t)n, inf_off, hf_off, bits, (uint64_t *)nullptr, rec_args(host_keys));
+    using K = void (*)(const DevKeyTable *, const uint8_t *, uint64_t, uint64_t, uint32_t, uint32_t, uint64_t *,
+                       uint64_t *, const RecArgs);
+    const bool ifid = keysel == HFV_KEYSEL_IFID;
+    K k = interleaved ? (ifid ? k_verify_records<HFV_KEYSEL_IFID, 0> : k_verify_records<HFV_KEYSEL_ZERO, 0>)
+                      : (ifid ? k_verify_records<HFV_KEYSEL_IFID, 1> : k_verify_records<HFV_KEYSEL_ZERO, 1>);
+    const unsigned grid = grid_for(n, kBlock, g.num_cus, 1);
+    hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0u, tab, recs, (uint64_t)stride, (uint64_t)n, inf_off, hf_off, bits,
+                          (uint64_t *)nullptr, rec_args(host_keys));
     return (int)hipGetLastError();
 }
 
 int launch_verify_stamped(const LaunchGeom &g, const DevKeyTable *tab, const DevKeyTable *host_keys, const uint8_t *recs,
-                          size_t n,
-                          uint64_t *bits, uint64_t *stamps, void *stream)
+                          size_t n, uint64_t *bits, uint64_t *stamps, void *stream)
 {
-    const KernelVariant &v = g.single;
-    unsigned grid = grid_for(n, 1024, g.num_cus, v.blocks_per_cu);
-    auto k = v.tab == 4 ? (v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 4, 1, 1, 1, 1>
-                                 : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 4, 1, 1, 1, 0>)
-                        : (v.dyn ? k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 1>
-                                 : k_verify_records<HFV_KEYSEL_ZERO, 1024, 1, 2, 1, 1, 1, 0>);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(1024), 0,
-                       (hipStream_t)stream, tab, (const uint32_t *)g.ttab_img, recs, (uint64_t)64, (uint64_t)n,
-                       (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits, stamps, rec_args(host_keys));
+    const unsigned grid = grid_for(n, kBlock, g.num_cus, 1);
+    hipLaunchKernelGGL((k_verify_records<HFV_KEYSEL_ZERO, 1, 1>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, tab,
+                       recs, (uint64_t)64, (uint64_t)n, (uint32_t)HFV_REC_INF_OFF, (uint32_t)HFV_REC_HF_OFF, bits,
+                       stamps, rec_args(host_keys));
     return (int)hipGetLastError();
 }
 
@@ -1779,68 +1212,20 @@ int launch_gen_records(const LaunchGeom &g, const DevKeyTable *tab, int keysel, 
     return (int)hipGetLastError();
 }
 
-// Persistent-grid geometry.  Defaults: see DESIGN.md section 4 (measured with
-// scripts/sweep.py).  HFV_KVARIANT="block=768,pf=2,tab=2,bpc=2" overrides the KEYSEL_ZERO
-// kernel and HFV_KVARIANT_IFID the per-lane-key kernel; blocks per CU are capped by the LDS
-// a block needs and by the occupancy query.
-static void parse_variant(const char *env, KernelVariant *v)
-{
-    if (!env) return;
-    const char *p = env;
-    while (*p) {
-        int val = 0;
-        if (sscanf(p, "block=%d", &val) == 1) v->block = val;
-        else if (sscanf(p, "pf=%d", &val) == 1) v->pf = val;
-        else if (sscanf(p, "tab=%d", &val) == 1) v->tab = val;
-        else if (sscanf(p, "bpc=%d", &val) == 1) v->blocks_per_cu = val;
-        else if (sscanf(p, "dma=%d", &val) == 1) v->dma = val;
-        else if (sscanf(p, "np=%d", &val) == 1) v->np = val;
-        else if (sscanf(p, "dyn=%d", &val) == 1) v->dyn = val;
-        else if (sscanf(p, "bs=%d", &val) == 1) v->bs = val;
-        const char *c = strchr(p, ',');
-        if (!c) break;
-        p = c + 1;
-    }
-}
-
-static int finish_variant(int keysel, KernelVariant *v)
-{
-    VerifyKernel k = keysel == HFV_KEYSEL_IFID ? pick_verify<HFV_KEYSEL_IFID>(*v) : pick_verify<HFV_KEYSEL_ZERO>(*v);
-    if (!k) return (int)hipErrorInvalidConfiguration;
-    int lds = (v->tab == 4 ? 131072 : 65536) + (keysel == HFV_KEYSEL_IFID ? (int)sizeof(uint4) * kDevKeyRows * HFV_MAX_KEYS + 32 : 0);
-    if (v->bs == kBsOnly) lds = (int)sizeof(s_bs);
-    else if (v->bs > 0) lds += (int)sizeof(s_bs);
-    int by_lds = (160 * 1024) / lds;
-    int by_waves = 32 / (v->block / 64);
-    int occ = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, v->block, 0);
-    if (e != hipSuccess) return (int)e;
-    int cap = by_lds < by_waves ? by_lds : by_waves;
-    if (occ > 0 && occ < cap) cap = occ;
-    if (cap < 1) cap = 1;
-    if (v->blocks_per_cu <= 0 || v->blocks_per_cu > cap) v->blocks_per_cu = cap;
-    return 0;
-}
-
-int build_ttab_image(uint32_t *img, void *stream)
-{
-    hipLaunchKernelGGL(k_build_ttab_image, dim3(kTtabImageDwords / 256), dim3(256), 0, (hipStream_t)stream, img);
-    return (int)hipGetLastError();
-}
-
 int query_geometry(int device, LaunchGeom *g)
 {
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return (int)e;
     g->num_cus = prop.multiProcessorCount;
-    g->single = KernelVariant{1024, 1, 4, 1, 1, 1, 1, 0};
-    g->multi = KernelVariant{1024, 1, 2, 1, 1, 1, 1, 0};
-    parse_variant(getenv("HFV_KVARIANT"), &g->single);
-    parse_variant(getenv("HFV_KVARIANT_IFID"), &g->multi);
-    int rc = finish_variant(HFV_KEYSEL_ZERO, &g->single);
-    if (rc) return rc;
-    return finish_variant(HFV_KEYSEL_IFID, &g->multi);
+    g->svc_blocks = g->num_cus;
+    // one 1024-thread block per CU must fit: the service's LDS (tables, config 3's key rows,
+    // descriptor cache) is the largest of the verify kernels'
+    int occ = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_verify_service<HFV_KEYSEL_IFID>, kBlock, 0);
+    if (e != hipSuccess) return (int)e;
+    if (occ < 1) return (int)hipErrorInvalidConfiguration;
+    return 0;
 }
 
 }  // namespace hfv

@@ -379,8 +379,7 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     // DMA in: each chunk's frame copy goes out in two halves on two streams (HIP gives each stream
     // its own copy-engine queue, and one engine does not fill the link: with a chunk on one
     // stream, runs landed at 166-172 or 213-265 Mpkt/s depending on the engines the streams got)
-    static const int split_env = getenv("HFV_LOOP_SPLIT") ? atoi(getenv("HFV_LOOP_SPLIT")) : 1;
-    const bool split = c->dma == 2 && split_env;
+    const bool split = c->dma == 2;
     uint64_t *dstats = nullptr;
     const size_t stats_bytes = HFV_BR_STATS_IFINDEX * 2 * HFV_BR_COUNTERS * 8;
     for (int i = 0; i < D && !rc && !host_stage; ++i) {

@@ -28,7 +28,7 @@ MAX_KEYS = 256
 REC_INF_OFF = 40
 REC_HF_OFF = 48
 REC_SIZE = 64
-SVC_RING = 256   # resident-service descriptor ring (kSvcRing, csrc/hfv_internal.h)
+SVC_RING = 128   # resident-service descriptor ring (kSvcRing, csrc/hfv_internal.h)
 SVC_INLINE = 64  # descriptors a service grid gets in its kernel arguments (kSvcInline)
 BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic HBM bytes per verified record
 
@@ -124,6 +124,7 @@ def lib():
         "hfv_last_error": (ctypes.c_char_p, []),
         "hfv_abi_version": (i32, []),
         "hfv_service_set_timing": (i32, [vp, i32]),
+        "hfv_service_set_grid": (i32, [vp, i32]),
         "aes_key_expansion": (None, [vp, vp]),
         "aes_cypher": (i32, [vp, vp, vp]),
         "aes_cmac_subkeys": (None, [vp, vp]),
@@ -393,8 +394,8 @@ class Ctx:
                                           _stream(stream)))
 
     def describe(self):
-        buf = ctypes.create_string_buffer(256)
-        _check(lib().hfv_ctx_describe(self._h, buf, 256))
+        buf = ctypes.create_string_buffer(512)
+        _check(lib().hfv_ctx_describe(self._h, buf, 512))
         return buf.value.decode()
 
     def attach_keymap(self, path):
@@ -620,6 +621,22 @@ class Ctx:
     def service_set_timing(self, enable):
         """Launch later service grids with (True) or without the dispatch timing events."""
         _check(lib().hfv_service_set_timing(self._h, 1 if enable else 0))
+
+    def service_set_grid(self, blocks):
+        """Later service grids use `blocks` blocks (0: one per CU) -- for ranks sharing one GPU."""
+        _check(lib().hfv_service_set_grid(self._h, int(blocks)))
+
+    def feed_loop(self, batches, depth=4):
+        """Diagnostic (hfv_debug_feed_loop): INTEGRATION.md section 2's data-plane loop run in C --
+        per batch one hfv_service_submit, hfv_service_wait on the ticket `depth` batches back --
+        returns its host wall time in seconds."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        L = lib()
+        L.hfv_debug_feed_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                          ctypes.POINTER(ctypes.c_uint64)]
+        ns = ctypes.c_uint64(0)
+        _check(L.hfv_debug_feed_loop(self._h, arr, len(arr), depth, ctypes.byref(ns)))
+        return ns.value * 1e-9
 
     @property
     def service_running(self):

@@ -2,7 +2,7 @@
 """Interleaved A/B of library builds on the bench headline (one bench.py process per run,
 HFV_LIB selecting the build):  python scripts/ab_libs.py ROUNDS lib1.so lib2.so[@VAR=VAL|...] ... [-- bench args]
 (a spec's @VAR=VAL|VAR2=VAL2 sets environment variables for that run: the same build with a switch;
-values may contain commas, e.g. lib.so@HFV_KVARIANT=block=512,bpc=2,tab=2)
+values may contain commas)
 Prints one line per run: build, value (Mpkt/s), grid ms, shader MHz, launch-path Mpkt/s."""
 import json
 import os

@@ -51,7 +51,7 @@ def test_two_product_ranks_on_one_gpu():
 @pytest.mark.gpu
 def test_two_service_ranks_on_one_gpu():
     """the service path with two ranks on GPU 0, each resident grid limited to
-    half the CUs (HFV_SVC_GRID = CUs / ranks), both timed together; every bitmap is checked
+    half the CUs (hfv_service_set_grid: CUs / ranks), both timed together; every bitmap is checked
     against the generator truth inside bench.py, and each rank reports its thread budget."""
     d = _bench("--gpus", "2", "--same-device", "--n", "262144", "--rotate", "2", "--steps", "8", "--warmup", "2",
                "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
@@ -62,10 +62,11 @@ def test_two_service_ranks_on_one_gpu():
     # per-rank grid times.  Each rank's grid verifies 8 x 2^18 records on half the
     # CUs side by side with the other's: about as long as one full-chip grid over 8 x 2^19
     # (~0.1 ms at 0.7 of 8 TB/s); neither rank's grid runs at the pace of host round trips (the
-    # round-3 fault: ~40 us per batch) and the two stay within 1.5x of each other.
+    # round-3 fault: ~40 us per batch; block_waits == 0 below is the deterministic check) and the
+    # two stay within 2.5x of each other (timing bounds loose: ADVICE r04).
     g = d["per_rank_ms"]["grid_ms"]
-    assert len(g) == 2 and all(0 < x < 0.3 for x in g), g
-    assert max(g) < 1.5 * min(g), g
+    assert len(g) == 2 and all(0 < x < 1.0 for x in g), g
+    assert max(g) < 2.5 * min(g), g
     assert all(r["block_waits"] == 0 for r in d["service"]["relay"]), d["service"]["relay"]
 
 

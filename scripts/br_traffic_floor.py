@@ -8,7 +8,8 @@ algorithmic bytes (exact bytes) and with PMC traffic (profiles/traffic.json br:1
 
 Round 2 counted the bytes past the window as a whole second 128-byte line; the PMC reads
 (157.4 B/frame) came in below that "floor" (160 B), which was therefore not one (VERDICT r02
-weak #3).  CPU only: python scripts/br_traffic_floor.py"""
+weak #3).  CPU only: python scripts/br_traffic_floor.py [PMC summary.json of scripts/pmc_round.sh br]
+(default: profiles/traffic.json's br:1048576 entry)."""
 import json
 import os
 import sys
@@ -39,18 +40,28 @@ def main():
         past = max(0, hdr - 128)                       # header bytes read past the window
         read_floor = 128 + 32 * -(-past // 32)
         read_64 = 128 + 64 * -(-past // 64)            # the same at the 64-byte request size of a miss
-        rows.append((abytes[i], read_floor + 32 * sectors + 12, read_floor, 32 * sectors, read_64))
+        rows.append((abytes[i], read_floor + 32 * sectors + 12, read_floor, 32 * sectors, read_64, hdr,
+                     abytes[i] - 12 - hdr))
     # bench.br_batch draws template ids uniformly over the flows (half good, half corrupted MACs
     # at 1/16) -- weight every template pair equally, as the batch does
     a = np.array(rows, dtype=float)
     good = np.array(good)
     w = np.where(good, 15 / 16, 1 / 16)
     w = w / w.sum()
-    alg, floor, rd, wr, rd64 = (float((a[:, j] * w).sum()) for j in range(5))
-    t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["br:1048576"]
-    pmc = t["hbm_bytes_per_launch"] / 2**20
-    prd, pwr = t["read_bytes"] / 2**20, t["write_bytes"] / 2**20
-    print(json.dumps({"algorithmic_bytes_per_frame": round(alg, 1), "granularity_floor_bytes_per_frame": round(floor, 1),
+    alg, floor, rd, wr, rd64, ard, awr = (float((a[:, j] * w).sum()) for j in range(7))
+    if len(sys.argv) > 1:   # a PMC summary (scripts/pmc_summary.py) of the same config-4 batch
+        t = json.load(open(sys.argv[1]))["1048576"]
+        prd, pwr = t["hbm_read_bytes_per_launch"] / 2**20, t["hbm_write_bytes_per_launch"] / 2**20
+        src = sys.argv[1]
+    else:
+        t = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["br:1048576"]
+        prd, pwr = t["read_bytes"] / 2**20, t["write_bytes"] / 2**20
+        src = "profiles/traffic.json br:1048576"
+    pmc = prd + pwr
+    print(json.dumps({"pmc_source": src,
+                      "algorithmic_bytes_per_frame": round(alg, 1), "algorithmic_read": round(ard + 6, 1),
+                      "algorithmic_write": round(awr + 6, 1),
+                      "granularity_floor_bytes_per_frame": round(floor, 1),
                       "floor_read": round(rd + 6, 1), "floor_write": round(wr + 6, 1),
                       "read_at_64B_requests": round(rd64 + 6, 1),
                       "pmc_bytes_per_frame": round(pmc, 1), "pmc_read": round(prd, 1), "pmc_write": round(pwr, 1),

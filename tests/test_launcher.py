@@ -54,8 +54,11 @@ def test_two_service_ranks_on_one_gpu():
     half the CUs (hfv_service_set_grid: CUs / ranks), both timed together; every bitmap is checked
     against the generator truth inside bench.py, and each rank reports its thread budget."""
     d = _bench("--gpus", "2", "--same-device", "--n", "262144", "--rotate", "2", "--steps", "8", "--warmup", "2",
-               "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
+               "--no-extras", "--no-host-e2e", "--cpu-budget", "0.2", timeout=600)
     assert d["n_gpus"] == 1 and d["ranks"] == 2 and len(d["per_rank_ms"]["all"]) == 2
+    # VERDICT r04 #6: the N > 1 line carries its CPU baseline (rank 0, after every rank's GPU legs)
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["verdicts_match_gpu"] is True, cb
     assert d["roofline"]["kernel"] == "k_verify_service" and d["value"] > 0
     assert int(d["same_device"]["service_grid_blocks"]) * 2 <= 256
     assert d["host_threads"]["ranks_on_node"] == 2 and d["host_threads"]["budget"] >= 1   # OMP_NUM_THREADS=1 here

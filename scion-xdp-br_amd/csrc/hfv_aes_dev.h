@@ -59,12 +59,6 @@ __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_
 // slower in the kernel (2^24 records: 257.5 vs 235.5 us, profiles/r01/addr_bitop3.log): the
 // verify loop is bound by LDS issue and the lookup chain's latency, not by VALU throughput,
 // and the second dependent instruction lengthens the address -> ds_read chain.
-// HFV_B1_BITOP3 = 1 (A/B builds only): byte-1 lookups addressed by the full-rate v_bitop3
-// form instead of v_perm (round 2: 8 % fewer VALU cycles, neutral at the ~2.0 GHz of a short
-// grid; VERDICT r04 #5 asks for it at the power-limited clock of a sustained one).
-#ifndef HFV_B1_BITOP3
-#define HFV_B1_BITOP3 0
-#endif
 struct Lane;
 template <int TAB, int K>
 __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l);
@@ -145,11 +139,7 @@ __device__ __forceinline__ uint32_t tlu(uint32_t w, uint32_t base, const Lane &l
         const uint32_t a3 = (__builtin_amdgcn_ubfe(w, 8 * K, 8) << (kTab3Log + 2)) | base;
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_tab32) + a3);
     }
-    uint32_t a;
-    if constexpr (HFV_B1_BITOP3 && K == 1)   // (w & 0xff00) | base: one full-rate v_bitop3_b32
-        a = __builtin_amdgcn_bitop3_b32(w, 0xff00u, base, 0xEA);
-    else
-        a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
+    const uint32_t a = __builtin_amdgcn_perm(w, base, K == 0 ? l.s0 : K == 1 ? l.s1 : K == 2 ? l.s2 : l.s3);
     const char *t = TAB == 4 ? reinterpret_cast<const char *>(s_tab128) : reinterpret_cast<const char *>(s_tab64);
     return *reinterpret_cast<const uint32_t *>(t + a);
 }

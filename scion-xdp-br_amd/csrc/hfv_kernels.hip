@@ -274,23 +274,11 @@ __device__ __forceinline__ uint64_t karg_cum(KArgs a, uint64_t k)
     return svc_cum(w, k);
 }
 
-// Experiment switches (A/B builds only, scripts/mkvar_k.sh; the defaults are the product):
-// HFV_SVC_NP = 2: a claim takes two consecutive tiles of the block's share, verified together
-// (two independent AES chains per wave); HFV_SVC_NT = 1: non-temporal record loads.
-#ifndef HFV_SVC_NP
-#define HFV_SVC_NP 1
-#endif
-#ifndef HFV_SVC_NT
-#define HFV_SVC_NT 0
-#endif
-constexpr uint32_t kSvcNP = HFV_SVC_NP;
-static_assert(kSvcNP == 1 || kSvcNP == 2, "tiles per claim");
-
 struct alignas(16) SvcSlot {
-    uint32_t base, count;   // block claim numbers [base, base + count); a claim is kSvcNP tiles
-    uint32_t done, stop;    // claims of the batch this block has verified; 1: exit descriptor
+    uint32_t base, count;   // block tile numbers [base, base + count)
+    uint32_t done, stop;    // tiles of the batch this block has verified; 1: exit descriptor
     uint64_t recs, bits, n, stride, tile0;   // the batch, and the first tile of the block's range
-    uint64_t ntiles;        // tiles of the block's range
+    uint64_t pad;
 };
 static __shared__ SvcSlot s_svc[kSvcRing];
 static __shared__ uint32_t s_svc_next, s_svc_loaded, s_svc_lock;
@@ -306,9 +294,9 @@ __device__ __forceinline__ void svc_share(uint64_t ntiles, uint64_t &t0, uint32_
     count = (uint32_t)(ntiles * s_svc_c1 / s_svc_w - t0);
 }
 
-struct SvcTile {   // one claim, wave-uniform
-    uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + kSvcNP * (g - base): its first tile
-    uint32_t b, base, count, ntiles;
+struct SvcTile {   // one claimed tile, wave-uniform
+    uint64_t recs, bits, n, stride, tile0, tile;   // tile = tile0 + (g - base)
+    uint32_t b, base, count;
 };
 enum SvcClaim { kSvcFound = 0, kSvcStop = 1, kSvcPending = 2 };
 
@@ -325,29 +313,12 @@ __device__ __forceinline__ RecWords load_tile(const SvcTile &t, uint32_t lane, u
     typedef const __attribute__((address_space(1))) u32x2 *P2;
     typedef const __attribute__((address_space(1))) uint32_t *P1;
     RecWords r;
-    u32x2 a, b;
-    if constexpr (HFV_SVC_NT) {
-        a = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
-        b = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
-        r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
-    } else {
-        a = *reinterpret_cast<P2>(p + inf_off);
-        b = *reinterpret_cast<P2>(p + hf_off);
-        r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
-    }
+    const u32x2 a = *reinterpret_cast<P2>(p + inf_off);
+    const u32x2 b = *reinterpret_cast<P2>(p + hf_off);
+    r.hfb = *reinterpret_cast<P1>(p + hf_off + 8);
     r.inf = make_uint2(a.x, a.y);
     r.hfa = make_uint2(b.x, b.y);
     return r;
-}
-
-// The claim's second tile (kSvcNP = 2), or its first again when the block's range has an odd
-// tile count and this is its last claim.
-__device__ __forceinline__ SvcTile second_tile(const SvcTile &t, bool &valid)
-{
-    SvcTile u = t;
-    valid = t.tile - t.tile0 + 1 < t.ntiles;
-    u.tile += valid ? 1 : 0;
-    return u;
 }
 
 __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
@@ -561,8 +532,7 @@ __device__ __attribute__((noinline)) bool svc_load(KArgs a, uint32_t b, bool blo
         svc_share((n + 63) / 64, t0, cnt);
         s.n = n;
         s.tile0 = t0;
-        s.ntiles = cnt;
-        s.count = (cnt + kSvcNP - 1) / kSvcNP;
+        s.count = cnt;
         if (s.count == 0) svc_complete(dev, a->tag, b);
     }
     __hip_atomic_store(&s_svc_loaded, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -591,8 +561,7 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
             cnt = (uint32_t)(nt * c1 / w - t0);
         }
     }
-    const uint32_t units = (cnt + kSvcNP - 1) / kSvcNP;   // claims
-    uint32_t incl = units;   // inclusive prefix sum of the claim counts over the lanes
+    uint32_t incl = cnt;   // inclusive prefix sum of the counts over the lanes
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
@@ -600,9 +569,8 @@ __device__ __attribute__((noinline)) void svc_load_inline(KArgs a, uint32_t lane
     }
     if (lane < n_in) {
         SvcSlot &s = s_svc[lane];
-        s.base = incl - units;
-        s.count = units;
-        s.ntiles = cnt;
+        s.base = incl - cnt;
+        s.count = cnt;
         s.done = 0;
         s.stop = stop;
         s.recs = d.recs;
@@ -638,7 +606,7 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
 {
     if (g - hint.base < hint.count) {   // same batch as the wave's current tile: no LDS reads
         t = hint;
-        t.tile = hint.tile0 + kSvcNP * (g - hint.base);
+        t.tile = hint.tile0 + (g - hint.base);
         return kSvcFound;
     }
     uint64_t t_wait = 0;
@@ -668,8 +636,7 @@ __device__ __forceinline__ SvcClaim svc_map(KArgs a, uint32_t lane, uint32_t g, 
             t.n = wave_uniform64(s.n);
             t.stride = wave_uniform64(s.stride);
             t.tile0 = wave_uniform64(s.tile0);
-            t.tile = t.tile0 + kSvcNP * (g - base);
-            t.ntiles = wave_uniform((uint32_t)s.ntiles);
+            t.tile = t.tile0 + (g - base);
             t.b = b;
             t.base = base;
             t.count = count;
@@ -795,9 +762,7 @@ __global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
                                __HIP_MEMORY_SCOPE_SYSTEM);
         stashed = 0;
     };
-    bool v2 = false;   // kSvcNP = 2: the current claim's second tile exists
-    RecWords rc = load_tile(cur, lane, inf_off, hf_off), rc2 = rc;
-    if constexpr (kSvcNP == 2) rc2 = load_tile(second_tile(cur, v2), lane, inf_off, hf_off);
+    RecWords rc = load_tile(cur, lane, inf_off, hf_off);
     svc_prefetch(a, lane, cur.b);
     for (;;) {
         // This tile's record words (and every earlier store) are complete.  An explicit wait
@@ -817,26 +782,15 @@ __global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
         SvcTile nx;
         SvcClaim c = svc_map(a, lane, g, false, mb, cur, nx);
         if (c != kSvcFound) nx = cur;
-        bool nv2 = false;
-        RecWords rn = load_tile(nx, lane, inf_off, hf_off), rn2 = rn;
-        if constexpr (kSvcNP == 2) rn2 = load_tile(second_tile(nx, nv2), lane, inf_off, hf_off);
-        uint64_t ballot = 0, ballot2 = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
-        if (keyok) {
-            ballot = verify_tile<KEYSEL>(rc, cur.tile * 64 + lane < cur.n, l, ukp);
-            if constexpr (kSvcNP == 2) ballot2 = verify_tile<KEYSEL>(rc2, (cur.tile + 1) * 64 + lane < cur.n, l, ukp);
-        }
+        RecWords rn = load_tile(nx, lane, inf_off, hf_off);
+        uint64_t ballot = 0;   // KEYSEL_ZERO with slot 0 empty: every packet fails closed
+        if (keyok) ballot = verify_tile<KEYSEL>(rc, cur.tile * 64 + lane < cur.n, l, ukp);
         if (lane == stashed) {
             st_word = ballot;
             st_tile = cur.tile;
         }
-        if constexpr (kSvcNP == 2) {   // the second tile's word, or the first's again (same address)
-            if (lane == stashed + 1) {
-                st_word = v2 ? ballot2 : ballot;
-                st_tile = cur.tile + (v2 ? 1 : 0);
-            }
-        }
         st_bits = cur.bits;
-        stashed += kSvcNP;
+        ++stashed;
         ++pending;
         const bool leave = c != kSvcFound || nx.b != cur.b;
         if (leave || stashed == 64) {
@@ -860,18 +814,13 @@ __global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
             }
             if (c == kSvcPending) {
                 c = svc_map(a, lane, g, true, mb, none, nx);
-                if (c == kSvcFound) {
-                    rn = load_tile(nx, lane, inf_off, hf_off);
-                    if constexpr (kSvcNP == 2) rn2 = load_tile(second_tile(nx, nv2), lane, inf_off, hf_off);
-                }
+                if (c == kSvcFound) rn = load_tile(nx, lane, inf_off, hf_off);
             }
         }
         if (c == kSvcStop) break;
         if (nx.b != cur.b) svc_prefetch(a, lane, nx.b);
         cur = nx;
         rc = rn;
-        rc2 = rn2;
-        v2 = nv2;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dev->run_clock[2] = __builtin_amdgcn_s_memtime();

@@ -1,8 +1,9 @@
 """Soak test of the resident service (diagnostic, not part of the pytest suites): many grids of
 random shape -- K batches of random, ragged sizes, some past the inline capacity and some past
 the ring -- through hfv_service_run, run_async and live submits, every bitmap compared with the
-launch path's on the same records.  Prints one line per 50 grids and a final count.
-Usage: python scripts/svc_soak.py [seconds] [seed]"""
+launch path's on the same records (whose own bitmap equals the generator's exact truth).
+Prints one line per 50 grids and a final count.
+Usage: python scripts/svc_soak.py [seconds] [seed] [zero|ifid]"""
 import os
 import random
 import sys
@@ -18,13 +19,15 @@ import bench  # noqa: E402
 SECONDS = float(sys.argv[1]) if len(sys.argv) > 1 else 60.0
 rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
 torch.cuda.set_device(0)
-ctx = bench.make_ctx(hfv, 0, hfv.KEYSEL_ZERO)
+KEYSEL = hfv.KEYSEL_IFID if len(sys.argv) > 3 and sys.argv[3] == "ifid" else hfv.KEYSEL_ZERO
+ctx = bench.make_ctx(hfv, 0, KEYSEL)
 N = 1 << 20
 recs = torch.empty((N, 64), dtype=torch.uint8, device="cuda")
 ctx.gen_records(recs, N, bench.SEED_RECORDS, first_index=0)
 ref = torch.zeros((N + 63) // 64, dtype=torch.int64, device="cuda")
 ctx.verify_records(recs, N, ref)
 torch.cuda.synchronize()
+assert torch.equal(ref, torch.from_numpy(bench.truth_bitmap(N, 0)).cuda()), "launch path != generator truth"
 ref_np = ref.cpu().numpy()
 
 

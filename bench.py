@@ -464,7 +464,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
 
 SUSTAINED_STEPS = 200   # batches per grid of the sustained leg (~2.3 ms each)
 SUSTAINED_GRIDS = 6     # back-to-back grids: the clock the power limit settles at under continuous load
-FEED_DEPTH = 4          # batches in flight in INTEGRATION.md section 2's feeder loop
+FEED_DEPTH = 8          # batches in flight in INTEGRATION.md section 2's feeder loop (scripts/svc_feed_depth.py)
 
 
 def service_legs(hfv, W, ctx, m, n, first, rotate, steps):

@@ -162,7 +162,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // One full round.  TAB = 2 expects the round key pre-rotated by 16 (device key image rows
 // 1..9) and folds it into the rotated half: 2 x xor3 + 1 rotate per column; TAB = 4 expects
 // the plain round key: 2 x xor3 per column.
-template <int TAB>
+template <int TAB, bool PIN = false>
 __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const Lane &l)
 {
     const uint32_t r[4] = {rk.x, rk.y, rk.z, rk.w};
@@ -183,6 +183,14 @@ __device__ __forceinline__ void round_full(uint32_t s[4], const uint4 &rk, const
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) s[c] = n[c];
+    if constexpr (TAB == 4 && PIN) {
+        // the round's issue order pinned: its 16 v_perm addresses, its 16 reads, its 8 xor3.
+        // Taken by the one-launch-per-batch kernel only: 17.2 against 17.8-19.1 us per 2^20
+        // batch there, neutral to slightly slower in the service (profiles/r05/s7/ab_sched_vk.log)
+        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);   // VALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);    // VALU
+    }
 }
 
 // Round 1 for a whitened macinput whose bytes 0,1,8,14,15 are key-only: the five lookups
@@ -348,7 +356,7 @@ __device__ __forceinline__ void cmac48_sched(const uint32_t w[4], uint32_t slot,
 }
 
 // Tag words 0..1 for a record-derived macinput w[] (bytes 0,1,8,14,15 zero).
-template <int TAB, class K>
+template <int TAB, class K, bool PIN = false>
 __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &key, const Lane &l, uint32_t &t0,
                                                 uint32_t &t1)
 {
@@ -356,7 +364,7 @@ __device__ __forceinline__ void cmac48_macinput(const uint32_t w[4], const K &ke
     uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
     round1_macinput<TAB>(s, key.row(11), l);
 #pragma unroll
-    for (int r = 2; r < 10; ++r) round_full<TAB>(s, key.template rk<TAB>(r), l);
+    for (int r = 2; r < 10; ++r) round_full<TAB, PIN>(s, key.template rk<TAB>(r), l);
     round_last_48<TAB>(s, key.row(10), l, t0, t1);
 }
 

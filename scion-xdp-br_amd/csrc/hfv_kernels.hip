@@ -96,14 +96,15 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
 // `in`: this lane's record exists.  KEYSEL_ZERO: the wave-uniform slot-0 key (the caller
 // handles an empty slot 0); KEYSEL_IFID: the slot's LDS rows, an empty slot fails closed
 // (xdp.c:83-84).
-template <int KEYSEL>
+// PIN: the round issue order of round_full (the launch kernel's choice, see there).
+template <int KEYSEL, bool PIN = false>
 __device__ __forceinline__ uint64_t verify_tile(const RecWords &r, bool in, const Lane &l, const UniformKey *ukey)
 {
     uint32_t w[4], t0, t1;
     rec_macinput(r, w);
     bool ok = in;
     if constexpr (KEYSEL == HFV_KEYSEL_ZERO) {
-        cmac48_macinput<4>(w, *ukey, l, t0, t1);
+        cmac48_macinput<4, UniformKey, PIN>(w, *ukey, l, t0, t1);
     } else {
         const uint32_t slot = rec_key_slot(r);
         cmac48_sched(w, slot, l, t0, t1);
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_verify_records(const DevKeyTable *__
             nt = t + stride_t;
         }
         RecWords nxt = load_rec(recs, stride, (b0 + nt) * 64 + lane, last, inf_off, hf_off);
-        const uint64_t ballot = verify_tile<KEYSEL>(cur, (b0 + t) * 64 + lane < n, l, &ukey);
+        const uint64_t ballot = verify_tile<KEYSEL, true>(cur, (b0 + t) * 64 + lane < n, l, &ukey);
         if (lane == stashed) {
             st_word = ballot;
             st_tile = b0 + t;

@@ -335,7 +335,6 @@ __device__ __forceinline__ uint4 next_round_key(const uint4 &rk, uint32_t t)
 __device__ __forceinline__ bool slot_valid(uint32_t slot) { return (s_valid[slot >> 5] >> (slot & 31)) & 1u; }
 
 // Tag words 0..1 of a record-derived macinput for the slot's key (s_keys5).
-template <bool PIN = false>
 __device__ __forceinline__ void cmac48_sched(const uint32_t w[4], uint32_t slot, const Lane &l, uint32_t &t0,
                                              uint32_t &t1)
 {
@@ -346,11 +345,11 @@ __device__ __forceinline__ void cmac48_sched(const uint32_t w[4], uint32_t slot,
     const uint32_t t[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     uint32_t s[4] = {w[0] ^ k0.x, w[1] ^ k0.y, w[2] ^ k0.z, w[3] ^ k0.w};
     round1_macinput<4>(s, r1, l);
-    round_full<4, PIN>(s, rk, l);
+    round_full<4>(s, rk, l);
 #pragma unroll
     for (int r = 3; r < 10; ++r) {
         rk = next_round_key(rk, t[r - 3]);
-        round_full<4, PIN>(s, rk, l);
+        round_full<4>(s, rk, l);
     }
     rk = next_round_key(rk, t[7]);                 // rk10
     round_last_48<4>(s, rk, l, t0, t1);

@@ -97,9 +97,6 @@ __device__ __forceinline__ bool rec_tag_matches(const RecWords &r, uint32_t t0, 
 // handles an empty slot 0); KEYSEL_IFID: the slot's LDS rows, an empty slot fails closed
 // (xdp.c:83-84).
 // PIN: the round issue order of round_full (the launch kernel's choice, see there).
-#ifndef HFV_IFID_PIN
-#define HFV_IFID_PIN 0   // A/B builds only (scripts/mkvar_k.sh -DHFV_IFID_PIN=1)
-#endif
 template <int KEYSEL, bool PIN = false>
 __device__ __forceinline__ uint64_t verify_tile(const RecWords &r, bool in, const Lane &l, const UniformKey *ukey)
 {
@@ -110,7 +107,7 @@ __device__ __forceinline__ uint64_t verify_tile(const RecWords &r, bool in, cons
         cmac48_macinput<4, UniformKey, PIN>(w, *ukey, l, t0, t1);
     } else {
         const uint32_t slot = rec_key_slot(r);
-        cmac48_sched<HFV_IFID_PIN != 0>(w, slot, l, t0, t1);
+        cmac48_sched(w, slot, l, t0, t1);
         ok = ok && slot_valid(slot);
     }
     return __ballot(ok && rec_tag_matches(r, t0, t1));

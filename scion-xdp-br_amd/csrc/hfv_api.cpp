@@ -254,6 +254,7 @@ struct hfv_ctx {
     bool svc_adapt = false;          // the running grid got all its batches up front (svc_run): measure it
     std::vector<uint64_t> svc_run_ns;   // ... their record counts
     struct timespec svc_launch_ts = {0, 0};   // host clock at the running grid's launch call
+    uint64_t svc_call_ns[6] = {0, 0, 0, 0, 0, 0};   // hfv_debug_service_call_ns: the last svc_run's phases
 };
 
 static int device_numa(int device, cpu_set_t *cpus);
@@ -1772,6 +1773,13 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
 
 static uint32_t g_svc_relay_delay_us = 0;   // hfv_debug_relay_delay
 
+static inline uint64_t mono_ns()
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
 static int svc_launch(hfv_ctx *ctx, DevState *ds)
 {
     const bool noev = !ctx->svc_timing;
@@ -1803,8 +1811,10 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     for (int r = 0; r < kDevKeyRows; ++r) memcpy(&a.key0[4 * r], ctx->host_img->keys.rows[r][0], 16);
     a.key0_ok = ctx->host_img->keys.valid[0] & 1u;
     memcpy(a.t0, kTables.t0, sizeof a.t0);
+    ctx->svc_call_ns[3] = mono_ns();
     int e = launch_verify_service(ctx->geom, ctx->keysel, a, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0],
                                   noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
+    ctx->svc_call_ns[4] = mono_ns();
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ++ctx->svc_launches;
@@ -1930,6 +1940,7 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
                    float *kernel_ms, bool wait)
 {
     if (!ctx || !first_ticket || (!batches && count)) return fail(-EINVAL, "null argument");
+    ctx->svc_call_ns[0] = mono_ns();
     *first_ticket = 0;
     if (kernel_ms) *kernel_ms = 0.0f;
     for (size_t i = 0; i < count; ++i) {
@@ -1944,8 +1955,10 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
     int rc = svc_quiesce(ctx);
     if (rc) return rc;
     DevState *ds;
+    ctx->svc_call_ns[1] = mono_ns();
     rc = svc_begin(ctx, ctx->svc_idle_ms, &ds);
     if (rc) return rc;
+    ctx->svc_call_ns[2] = mono_ns();
     ctx->svc_adapt = true;   // every batch is in the ring before the grid starts: measure its balance
     ctx->svc_run_ns.resize(count);
     for (size_t i = 0; i < count; ++i) ctx->svc_run_ns[i] = batches[i].n;
@@ -1973,6 +1986,7 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
         int lr = svc_launch(ctx, ds);
         if (lr) return lr;
     }
+    ctx->svc_call_ns[5] = mono_ns();
     if (!wait) return rc;   // the grid exits after the stop posted behind the batches
     int sr = svc_stop(ctx, kernel_ms);
     return rc ? rc : sr;
@@ -2112,6 +2126,18 @@ int hfv_debug_feed_loop(hfv_ctx *ctx, const struct hfv_batch *b, size_t count, u
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     *ns = (uint64_t)((t1.tv_sec - t0.tv_sec) * 1000000000ll + (t1.tv_nsec - t0.tv_nsec));
+    return 0;
+}
+
+// Diagnostic (not part of include/scion_hfv.h): the host-side phases of the last
+// hfv_service_run / run_async call in nanoseconds: [0] argument checks and stopping a previous
+// grid, [1] the new grid's bookkeeping (svc_begin), [2] posting the batches and building the
+// kernel arguments, [3] the launch call itself, [4] the rest (ticket state) to the return.
+int hfv_debug_service_call_ns(hfv_ctx *ctx, uint64_t out[5])
+{
+    if (!ctx || !out) return fail(-EINVAL, "bad argument");
+    const uint64_t *c = ctx->svc_call_ns;
+    for (int i = 0; i < 5; ++i) out[i] = c[i + 1] >= c[i] ? c[i + 1] - c[i] : 0;
     return 0;
 }
 

@@ -677,7 +677,7 @@ template <int KEYSEL>
 __global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
 {
     // the fields through the kernarg segment pointer (constant address space): no private copy
-    // of the 2.4 KB argument struct, and helpers take the pointer
+    // of the 3.3 KiB argument struct, and helpers take the pointer
     const KArgs a = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     (void)args;
     const uint32_t lane = threadIdx.x & 63;

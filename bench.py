@@ -80,7 +80,7 @@ HBM_ACHIEVABLE_GBS = 6500.0      # a pure streaming read of the records' access 
 BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic bytes per verified record
 M64 = (1 << 64) - 1
 # committed PMC summary of the headline configuration (scripts/pmc_round.sh ... svc rot)
-PMC_SUMMARY = {"zero": "profiles/r04/final5/pmc_zero_svc/summary.json", "ifid": "profiles/r05/pmc_ifid_svc/summary.json"}
+PMC_SUMMARY = {"zero": "profiles/r05/final/pmc_zero_svc/summary.json", "ifid": "profiles/r05/pmc_ifid_svc/summary.json"}
 METRIC = "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets"
 
 

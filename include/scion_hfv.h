@@ -180,7 +180,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
  * (border_router, xdp.c:250-284, runs for every packet without a per-packet load): one
  * persistent grid per ctx keeps the AES tables (and, for KEYSEL_IFID, the key image)
  * resident in LDS and verifies batches as the host posts them, with the same verdict
- * semantics as hfv_verify_records.  Batches are posted into a 256-entry descriptor ring in
+ * semantics as hfv_verify_records.  Batches are posted into a 128-entry descriptor ring in
  * pinned host memory; no kernel launch or table fill per batch, and a batch's tail
  * overlaps the next batch's start.  Batches posted before the grid starts (hfv_service_run /
  * run_async, submitv on a stopped service) travel in the launch's kernel arguments (up to 64),
@@ -198,7 +198,7 @@ int hfv_verify_records_host(hfv_ctx *ctx, const void *recs, size_t stride, size_
 /* Launch the service grid (no-op if running).  idle_ms 0: 1000 ms. */
 int hfv_service_start(hfv_ctx *ctx, uint32_t idle_ms);
 /* Post one batch (device pointers, as hfv_verify_records; starts the service if needed).
- * Returns its ticket (1, 2, ...) in *ticket.  Blocks only while 256 batches are in flight.
+ * Returns its ticket (1, 2, ...) in *ticket.  Blocks only while 128 batches are in flight.
  * Host-ordered, not stream-ordered: the records must be in place and the bitmap must no
  * longer be written by other work when the call is made (synchronize their producers). */
 int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,

@@ -782,8 +782,7 @@ __device__ __forceinline__ void br_frame(BrFrame &k, uint64_t i, const DevKeyTab
 // wave instruction... 64 / (WIN / 16) frames per instruction), staged in LDS and parsed from
 // there, and the next tile's bytes are already in flight while this one is parsed.
 template <int BLOCK, bool STATS, int WIN>
-__global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st,
-                                                      const uint32_t *__restrict__ ttab_img, const uint8_t *pkts,
+__global__ __launch_bounds__(BLOCK) void k_br_process(const DevState *__restrict__ st, const uint8_t *pkts,
                                                       uint8_t *out,
                                                       uint64_t slot, uint32_t maxlen, uint32_t window,
                                                       const uint16_t *__restrict__ lens,
@@ -1026,7 +1025,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     // (the staged loop addresses a tile of 64 slots through 32-bit buffer offsets: 64 * slot < 2^31)
     bool staged = slot >= (size_t)kBrWin && slot % 16 == 0 && ((uintptr_t)pkts & 15) == 0 &&
                   ((uintptr_t)out & 15) == 0 && slot < ((size_t)1 << 25);
-    using K = void (*)(const DevState *, const uint32_t *, const uint8_t *, uint8_t *, uint64_t, uint32_t, uint32_t,
+    using K = void (*)(const DevState *, const uint8_t *, uint8_t *, uint64_t, uint32_t, uint32_t,
                        const uint16_t *,
                        const uint32_t *, uint64_t, uint8_t *, uint8_t *, int32_t *, unsigned long long *);
     K k;
@@ -1064,7 +1063,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
     unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
     if (g_br_grid_override && g_br_grid_override < grid) grid = g_br_grid_override;
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0u, st, (const uint32_t *)nullptr, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
+                          (hipEvent_t)ev_stop, 0u, st, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,
                           (unsigned long long *)stats);
     return (int)hipGetLastError();

@@ -376,6 +376,33 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
 
     out = {"launch_el": launch_el, "k_mean": k_mean, "k_med": k_med, "batches": batches, "bitmaps": bitmaps,
            "svc_el": None, "per_rank_s": None, "grid_ms": None, "mhz": None}
+
+    # --- stream-ordered batch list: the K batches in one hfv_verify_batches call (one launch per
+    # 64 batches), table fill and grid ramp paid once; the region's closing synchronize waits ---
+    blist = ctx.service_batches([(batches[k % R], n, bitmaps[k % nb]) for k in range(steps)])
+    run_b = ctx.verify_batches_fn(blist, stream=stream)
+    for b in bitmaps:
+        b.zero_()
+    run_b()
+    W.sync()
+    check(max(R, steps))
+    b_runs = []
+    for _ in range(max(1, reps)):
+        for b in bitmaps:
+            b.zero_()
+        W.sync()
+        b_runs.append(W.timed(1, run_b))
+        check(steps)
+    b_runs.sort(key=lambda r: r[0])
+    b_ms = []
+    for _ in range(max(1, reps)):   # (kernel ms, block 0's shader clock) per event-timed call
+        b_ms.append((ctx.verify_batches_timed(blist, stream=stream), ctx.batches_shader_mhz()))
+    check(steps)
+    b_med = sorted(b_ms)[len(b_ms) // 2]
+    out.update({"bat_el": b_runs[len(b_runs) // 2][0], "bat_per_rank_s": b_runs[len(b_runs) // 2][1],
+                "bat_all_ms": [round(r[0] * 1e3, 4) for r in b_runs], "bat_kernel_ms": b_med[0],
+                "bat_mhz": b_med[1], "bat_all_kernel_ms": [round(x[0], 4) for x in b_ms],
+                "bat_all_mhz": [round(x[1], 1) if x[1] else None for x in b_ms]})
     if not service:
         out["per_rank_s"] = W.gather(launch_el)
         return out
@@ -963,10 +990,21 @@ def run_hf(args, W):
     # an extra leg (host threads, PCIe copies) while another is still in its headline regions
     per_rank_grid = W.gather(m["grid_ms"] or 0.0)
     W.barrier()
-    headline = "launch" if args.launch_only else args.mode
-    elapsed = m["svc_el"] if headline == "service" else m["launch_el"]
+    headline = "launch" if args.launch_only and args.mode == "service" else args.mode
+    elapsed = {"service": m["svc_el"], "launch": m["launch_el"], "batches": m["bat_el"]}[headline]
+    if headline == "batches":
+        m["per_rank_s"] = m["bat_per_rank_s"]
     bytes_per_batch = BYTES_PER_PACKET * n
-    if headline == "service":
+    if headline == "batches":
+        achieved = bytes_per_batch * args.steps / (m["bat_kernel_ms"] * 1e-3) / 1e9
+        kern = {"kernel": "k_verify_batches", "kernel_ms": round(m["bat_kernel_ms"], 4),
+                "batches_per_call": args.steps, "launches": -(-args.steps // 64),
+                "kernel_ms_per_batch": round(m["bat_kernel_ms"] / args.steps, 5),
+                "algorithmic_bytes_per_batch": int(bytes_per_batch),
+                "timing": "dispatch start/stop events (hipExtLaunchKernel) of the call's launches, in calls identical "
+                          "to the value's but for the events (median)"}
+        traffic = pmc_traffic(f"bat:{args.keysel}:{n}:rot{args.rotate}")
+    elif headline == "service":
         achieved = bytes_per_batch * args.steps / (m["grid_ms"] * 1e-3) / 1e9
         kern = {"kernel": "k_verify_service", "grid_ms": round(m["grid_ms"], 4), "batches_per_grid": args.steps,
                 "kernel_ms_per_batch": round(m["grid_ms"] / args.steps, 5),
@@ -1006,12 +1044,22 @@ def run_hf(args, W):
                          variant=ctx.describe(),
                          note=f"step k verifies resident batch k % {args.rotate} ({args.rotate} x {n * 64 >> 20} MiB "
                               f"per GPU > 256 MiB Infinity Cache): records are read from HBM"),
-        "ceilings": ceilings(args.keysel, n, m["mhz"], cus),
-        "path": ("resident service: one persistent grid; the K batches and a stop descriptor posted through the "
-                 "host descriptor ring by one hfv_service_run_async call, which launches the grid after them; the "
-                 "timed region's closing device synchronize waits for the grid to exit; posting, grid launch, table "
-                 "fill and drain inside the timed region"
-                 if headline == "service" else "one hfv_verify_records launch per batch"),
+        "ceilings": ceilings(args.keysel, n, m["bat_mhz"] if headline == "batches" else m["mhz"], cus),
+        "path": {"service": "resident service: one persistent grid; the K batches and a stop descriptor posted "
+                            "through the host descriptor ring by one hfv_service_run_async call, which launches the "
+                            "grid after them; the timed region's closing device synchronize waits for the grid to "
+                            "exit; posting, grid launch, table fill and drain inside the timed region",
+                 "batches": "stream-ordered batch list: the K batches in one hfv_verify_batches call on the rank's "
+                            "stream (one launch per 64 batches: table fill, ramp and tail paid once per launch); the "
+                            "timed region's closing device synchronize waits for it",
+                 "launch": "one hfv_verify_records launch per batch"}[headline],
+        "batches": {"mpkts": round(total * args.steps / m["bat_el"] / 1e6, 2),
+                    "ms_per_step": round(m["bat_el"] / args.steps * 1e3, 5),
+                    "kernel_ms": round(m["bat_kernel_ms"], 4),
+                    "frac": round(bytes_per_batch * args.steps / (m["bat_kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "timed_regions_ms": m["bat_all_ms"], "kernel_ms_all": m["bat_all_kernel_ms"],
+                    "shader_mhz": round(m["bat_mhz"], 1) if m["bat_mhz"] else None, "mhz_all": m["bat_all_mhz"],
+                    "path": "hfv_verify_batches: K batches, one stream-ordered launch per 64"},
         "service": None if args.launch_only else {
             "mpkts": round(total * args.steps / m["svc_el"] / 1e6, 2),
             "ms_per_step": round(m["svc_el"] / args.steps * 1e3, 5), "grid_ms": round(m["grid_ms"], 4),
@@ -1175,8 +1223,9 @@ def main():
     ap.add_argument("--loop-dma", type=int, default=2, choices=(0, 1, 2),
                     help="config-5 loop router I/O: 0 zero-copy over PCIe, 1 DMA through HBM both ways, "
                          "2 DMA in + the kernel writing its changes into the ring")
-    ap.add_argument("--mode", choices=["service", "launch"], default="service",
-                    help="hf headline: resident service grid (default) or one launch per batch")
+    ap.add_argument("--mode", choices=["service", "launch", "batches"], default="service",
+                    help="hf headline: resident service grid (default), one launch per batch, or the K batches "
+                         "in one stream-ordered hfv_verify_batches call")
     ap.add_argument("--settle-s", type=float, default=0.5, help="idle seconds before each extra leg (untimed)")
     ap.add_argument("--svc-reps", type=int, default=5, help="timed service regions of K steps (median reported; 5: robust to two host hiccups)")
     ap.add_argument("--launch-only", action="store_true",

@@ -142,6 +142,26 @@ int hfv_ctx_attach_keymap(hfv_ctx *ctx, const char *path);
  * recs: n records of `stride` bytes (8-byte aligned, stride % 8 == 0). */
 int hfv_verify_records(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, uint64_t *pass_bits,
                        void *stream);
+/* One batch of records for the multi-batch calls (hfv_verify_batches, hfv_service_submitv,
+ * hfv_service_run): n records of `stride` bytes at recs, verdicts into pass_bits. */
+struct hfv_batch {
+    const void *recs;
+    size_t stride;
+    size_t n;
+    uint64_t *pass_bits;
+};
+/* hfv_verify_records over `count` batches in ONE stream-ordered launch (up to 64 batches per
+ * launch; more are split): the round tables are written into LDS once for all of them, and
+ * the batches' tiles are dealt to the CUs as one contiguous range.  Records written by earlier
+ * work on `stream` are read, the bitmaps are complete for later work on it -- the fast path
+ * for callers whose batches come from a copy or a parse kernel on a stream (one
+ * hfv_verify_records launch per batch pays the table fill and the grid's ramp and tail per
+ * batch).  Each batch is checked as hfv_verify_records checks one; empty batches are skipped. */
+int hfv_verify_batches(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, void *stream);
+/* Same, then waits and stores the launches' execution time (dispatch start of the first to
+ * dispatch end of the last) in *kernel_ms.  For benchmarks. */
+int hfv_verify_batches_timed(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, void *stream,
+                             float *kernel_ms);
 /* Verdict counts for the verify-only paths, modelled on record_verdict (xdp.c:54-70) but NOT
  * its layout: counters[slot][0] += packets that verified, counters[slot][1] += packets dropped
  * as VERDICT_INVALID_HF, where slot is the packet's AS-ingress interface (IFID & 0xff,
@@ -206,12 +226,6 @@ int hfv_service_submit(hfv_ctx *ctx, const void *recs, size_t stride, size_t n, 
 /* Post `count` batches in one call (tickets *first_ticket .. *first_ticket + count - 1), the
  * many-descriptor form of hfv_service_submit (recvmmsg-style: one call per burst of RX
  * batches).  All batches are checked before any is posted. */
-struct hfv_batch {
-    const void *recs;
-    size_t stride;
-    size_t n;
-    uint64_t *pass_bits;
-};
 int hfv_service_submitv(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, uint64_t *first_ticket);
 /* One-shot run: the batches on a fresh grid (a running service is stopped first), with the
  * stop descriptor posted right behind them, so the grid exits as soon as the last batch is

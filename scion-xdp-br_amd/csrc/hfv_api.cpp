@@ -207,6 +207,7 @@ struct hfv_ctx {
     uint32_t brmap_seq = 0xffffffffu;
     // dispatch timing (hfv_verify_records_timed)
     hipEvent_t tev[2] = {nullptr, nullptr};
+    uint64_t *bat_clk = nullptr;   // device: hfv_verify_batches' block-0 clock stamps (hfv_debug_batches_clock)
     // router tables for hfv_br_process (published with the key table)
     DevBrConfig br{};
     hfv_br_config cfg_src{};   // the tables as installed (checked against the build options)
@@ -441,6 +442,8 @@ int hfv_ctx_create(int device, hfv_ctx **out)
                 if (hipEventCreateWithFlags(&c->reader_ev[i][r], hipEventDisableTiming) != hipSuccess) rc = -EIO;
         }
         if (rc) break;
+        if (hipMalloc((void **)&c->bat_clk, kBatchClkWords * sizeof(uint64_t)) != hipSuccess) { rc = -ENOMEM; break; }
+        if (hipMemset(c->bat_clk, 0, kBatchClkWords * sizeof(uint64_t)) != hipSuccess) { rc = -EIO; break; }
         if (query_geometry(device, &c->geom) != 0) {
             hfv_ctx_destroy(c);
             return fail(-EINVAL, "device %d cannot hold a 1024-thread verify block with 156 KiB of LDS", device);
@@ -488,6 +491,7 @@ int hfv_ctx_destroy(hfv_ctx *ctx)
     }
     if (ctx->brh_dstats) (void)hipFree(ctx->brh_dstats);
     if (ctx->zc_meta) (void)hipFree(ctx->zc_meta);
+    if (ctx->bat_clk) (void)hipFree(ctx->bat_clk);
     keymap_close(ctx->keymap);
     brcfg_close(ctx->brmap);
     for (int i = 0; i < 2; ++i)
@@ -681,6 +685,116 @@ int hfv_verify_records_timed(hfv_ctx *ctx, const void *recs, size_t stride, size
     if (rc) return rc;
     HIP_TRY(hipEventSynchronize(ctx->tev[1]));
     HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
+// The batch list of hfv_verify_batches: checked as hfv_verify_records checks one batch; empty
+// batches are dropped.
+static int batches_check(const hfv_ctx *ctx, const struct hfv_batch *b, size_t count)
+{
+    if (!b && count) return fail(-EINVAL, "null batch list");
+    for (size_t i = 0; i < count; ++i) {
+        if (b[i].n == 0) continue;
+        if (!b[i].recs || !b[i].pass_bits) return fail(-EINVAL, "batch %zu: null buffer", i);
+        if (((uintptr_t)b[i].recs & 7) || (b[i].stride & 7) || ((uintptr_t)b[i].pass_bits & 7))
+            return fail(-EINVAL, "batch %zu: records, stride and bitmap must be 8-byte aligned", i);
+        if (b[i].stride < (size_t)ctx->inf_off + 8 || b[i].stride < (size_t)ctx->hf_off + 12)
+            return fail(-EINVAL, "batch %zu: stride %zu too small for INF@%u/HF@%u", i, b[i].stride, ctx->inf_off,
+                        ctx->hf_off);
+        if (b[i].stride > (1u << 24)) return fail(-EINVAL, "batch %zu: stride %zu > 16 MiB", i, b[i].stride);
+        if (b[i].n > ((size_t)1 << 36)) return fail(-EINVAL, "batch %zu: %zu records (at most 2^36)", i, b[i].n);
+    }
+    return 0;
+}
+
+// One launch per kBatchMax non-empty batches (and at most 2^31 tiles); ev0/ev1 (nullable) bracket
+// the first and the last launch.
+static int batches_launch(hfv_ctx *ctx, const struct hfv_batch *b, size_t count, hipStream_t st, hipEvent_t ev0,
+                          hipEvent_t ev1)
+{
+    DevState *ds;
+    int rc = publish_keys(ctx, st, &ds);
+    if (rc) return rc;
+    BatchArgs a;
+    memset(&a, 0, sizeof a);
+    a.tab = &ds->keys;
+    a.inf_off = ctx->inf_off;
+    a.hf_off = ctx->hf_off;
+    a.clk = ctx->bat_clk;
+    for (int r = 0; r < kDevKeyRows; ++r) memcpy(&a.key0[4 * r], ctx->host_img->keys.rows[r][0], 16);
+    a.key0_ok = ctx->host_img->keys.valid[0] & 1u;
+    memcpy(a.t0, kTables.t0, sizeof a.t0);
+    size_t last = count;   // the last non-empty batch: its launch records ev1
+    while (last > 0 && b[last - 1].n == 0) --last;
+    bool first = true;
+    for (size_t i = 0; i < last;) {
+        a.nb = 0;
+        uint64_t tiles = 0;
+        for (; i < last && a.nb < kBatchMax; ++i) {
+            if (b[i].n == 0) continue;
+            const uint64_t t = (b[i].n + 63) / 64;
+            if (a.nb && tiles + t > (1ull << 31)) break;
+            a.d[a.nb] = {(uint64_t)(uintptr_t)b[i].recs, (uint64_t)(uintptr_t)b[i].pass_bits, (uint64_t)b[i].n,
+                         (uint64_t)b[i].stride};
+            a.cum[a.nb] = (uint32_t)tiles;
+            tiles += t;
+            ++a.nb;
+        }
+        a.cum[a.nb] = (uint32_t)tiles;
+        a.total = (uint32_t)tiles;
+        const bool fin = i >= last;
+        int e = launch_verify_batches(ctx->geom, ctx->keysel, a, st, first ? ev0 : nullptr, fin ? ev1 : nullptr);
+        rc = after_launch(ctx, st, e, "verify_batches launch");
+        if (rc) return rc;
+        first = false;
+    }
+    return 0;
+}
+
+int hfv_verify_batches(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, void *stream)
+{
+    if (!ctx) return fail(-EINVAL, "ctx is NULL");
+    int rc = batches_check(ctx, batches, count);
+    if (rc) return rc;
+    DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
+    return batches_launch(ctx, batches, count, pick_stream(ctx, stream), nullptr, nullptr);
+}
+
+int hfv_verify_batches_timed(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, void *stream,
+                             float *kernel_ms)
+{
+    if (!ctx || !kernel_ms) return fail(-EINVAL, "null argument");
+    *kernel_ms = 0.0f;
+    int rc = batches_check(ctx, batches, count);
+    if (rc) return rc;
+    size_t nonempty = 0;
+    for (size_t i = 0; i < count; ++i) nonempty += batches[i].n != 0;
+    if (!nonempty) return 0;
+    DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
+    for (int i = 0; i < 2; ++i)
+        if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
+    // the block finish stamps are atomic maxima: cleared before the timed launches (outside the events)
+    HIP_TRY(hipMemsetAsync(ctx->bat_clk + 4 + kBatchStampBlocks, 0, kBatchStampBlocks * sizeof(uint64_t),
+                           pick_stream(ctx, stream)));
+    rc = batches_launch(ctx, batches, count, pick_stream(ctx, stream), ctx->tev[0], ctx->tev[1]);
+    if (rc) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->tev[1]));
+    HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
+// Diagnostic (not part of include/scion_hfv.h): block 0's shader clock (s_memtime) and 100 MHz
+// s_memrealtime at the start and at the end of the last hfv_verify_batches launch (out[0..3]);
+// with words >= 4 + 2 * 1024 also every block's s_memrealtime after its table fill (out[4 + k]) and
+// when it finished (out[4 + 1024 + k]).  The caller has synchronized that launch.
+extern "C" int hfv_debug_batches_clock(hfv_ctx *ctx, uint64_t *out, size_t words)
+{
+    if (!ctx || !out || words < 4) return fail(-EINVAL, "bad argument");
+    DeviceGuard g(ctx->device);
+    if (words > kBatchClkWords) words = kBatchClkWords;
+    HIP_TRY(hipMemcpy(out, ctx->bat_clk, words * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -258,6 +258,29 @@ static_assert(sizeof(SvcArgs) <= 4096, "SvcArgs exceeds the 4 KiB kernel-argumen
 static_assert(sizeof(RecArgs) + 128 <= 4096, "RecArgs and the launch's other arguments exceed 4 KiB");
 int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid);
+// Stream-ordered batch list (hfv_verify_batches): up to kBatchMax batches per launch, their
+// descriptors and the running tile count cum[] (batch j = global tiles [cum[j], cum[j+1]),
+// cum[nb] = total) in the one by-value kernel argument, beside T0 and the slot-0 key rows.
+constexpr uint32_t kBatchMax = 64;
+constexpr uint32_t kBatchStampBlocks = 1024;
+constexpr size_t kBatchClkWords = 4 + 2 * kBatchStampBlocks;
+struct BatchArgs {
+    const DevKeyTable *tab;
+    uint32_t inf_off, hf_off;
+    uint32_t nb, total;       // batches; tiles over all of them (< 2^32: 288 GB of records at stride 8 is 2^29 tiles)
+    // nullable (diagnostics): [0..3] block 0's s_memtime / s_memrealtime at its start and at its end
+    // (wave 0); [4 + k] block k's s_memrealtime after its table fill, [4 + kBatchStampBlocks + k]
+    // when its last wave left (atomic max: the host zeroes it before the launch)
+    uint64_t *clk;
+    uint32_t key0[kDevKeyRows * 4];
+    uint32_t key0_ok, pad_[3];
+    uint32_t t0[256];
+    SvcDescLite d[kBatchMax];
+    uint32_t cum[kBatchMax + 1];
+};
+static_assert(sizeof(BatchArgs) <= 4096, "BatchArgs exceeds the 4 KiB kernel-argument segment");
+int launch_verify_batches(const LaunchGeom &g, int keysel, const BatchArgs &args, void *stream, void *ev_start,
+                          void *ev_stop);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

@@ -227,6 +227,173 @@ __global__ __launch_bounds__(kBlock) void k_verify_records(const DevKeyTable *__
 }
 
 // ---------------------------------------------------------------------------------------
+// stream-ordered batch list (hfv_verify_batches): up to kBatchMax batches in ONE launch
+// ---------------------------------------------------------------------------------------
+// The batches' tiles are numbered one after the other (batch j holds global tiles
+// [cum[j], cum[j+1])) and block k verifies the contiguous range [T*k/G, T*(k+1)/G) of that
+// space, its waves claiming tiles from an LDS counter as k_verify_records does.  A block's
+// range spans one or two batches, so a wave changes batch about once per block range: the
+// batch's descriptor sits in SGPRs, read from the kernel arguments (scalar loads) only when a
+// claim leaves it.  Against the resident service (k_verify_service) this launch has no relay
+// wave, no completion protocol and no system-scope verdict stores (the launch is stream
+// ordered: the kernel's end publishes the bitmaps), and it pays the table fill once for all
+// of its batches instead of once per batch as a launch per batch does.
+typedef const __attribute__((address_space(4))) BatchArgs *BArgs;
+
+struct BatchTile {   // the wave's current batch (wave-uniform)
+    uint64_t recs, bits, n, stride;
+    uint32_t lo, hi;   // its global tiles [lo, hi)
+    uint32_t j;
+};
+
+__device__ __forceinline__ void batch_enter(BArgs a, uint32_t j, BatchTile &b)
+{
+    b.j = j;
+    b.recs = a->d[j].recs;
+    b.bits = a->d[j].bits;
+    b.n = a->d[j].n;
+    b.stride = a->d[j].stride;
+    b.lo = a->cum[j];
+    b.hi = a->cum[j + 1];
+}
+
+// global tile g -> its batch (g only grows along a wave's claims; g < a->total)
+__device__ __forceinline__ void batch_map(BArgs a, uint32_t g, BatchTile &b)
+{
+    if (g < b.hi) return;
+    uint32_t j = b.j + 1;
+    while (g >= a->cum[j + 1]) ++j;
+    batch_enter(a, j, b);
+}
+
+__device__ __forceinline__ RecWords batch_load(const BatchTile &b, uint32_t g, uint32_t lane, uint32_t inf_off,
+                                               uint32_t hf_off)
+{
+    const uint64_t first = (uint64_t)(g - b.lo) * 64;
+    const uint64_t left = b.n - 1 - first;                      // uniform: last valid lane
+    const uint32_t lim = left < 63 ? (uint32_t)left : 63u;
+    const uint32_t off = (lane < lim ? lane : lim) * (uint32_t)b.stride;
+    const GlobalU8 *p = (const GlobalU8 *)(b.recs + first * b.stride) + off;
+    typedef const __attribute__((address_space(1))) u32x2 *P2;
+    typedef const __attribute__((address_space(1))) uint32_t *P1;
+    RecWords r;
+    const u32x2 x = __builtin_nontemporal_load(reinterpret_cast<P2>(p + inf_off));
+    const u32x2 y = __builtin_nontemporal_load(reinterpret_cast<P2>(p + hf_off));
+    r.hfb = __builtin_nontemporal_load(reinterpret_cast<P1>(p + hf_off + 8));
+    r.inf = make_uint2(x.x, x.y);
+    r.hfa = make_uint2(y.x, y.y);
+    return r;
+}
+
+// DEPTH: tiles whose record loads are in flight ahead of the one being verified (1: the next
+// tile's, as k_verify_records; 2: the next two -- HFV_BATCH_DEPTH, an A/B build switch).  Every
+// load is issued unconditionally (a claim past the block's range re-reads its last tile), so the
+// waitcnt pass keeps a counted vmcnt for the tiles still ahead instead of a vmcnt(0).
+#ifndef HFV_BATCH_DEPTH
+#define HFV_BATCH_DEPTH 1
+#endif
+template <int KEYSEL, int DEPTH>
+__global__ __launch_bounds__(kBlock) void k_verify_batches(const BatchArgs args)
+{
+    static_assert(DEPTH == 1 || DEPTH == 2, "prefetch depth");
+    const BArgs a = (BArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)args;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = wave_uniform(threadIdx.x / 64);
+    const uint32_t total = a->total;
+    const uint32_t b0 = (uint32_t)((uint64_t)total * blockIdx.x / gridDim.x);
+    const uint32_t b1 = (uint32_t)((uint64_t)total * (blockIdx.x + 1) / gridDim.x);
+    if (b1 == b0) return;   // (the launcher gives every block at least one tile)
+    const uint32_t last = b1 - 1;
+    const uint32_t inf_off = a->inf_off, hf_off = a->hf_off;
+    UniformKey ukey(a->key0, a->key0_ok);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a->clk) {   // diagnostics: the shader clock over the grid
+        a->clk[0] = __builtin_amdgcn_s_memtime();
+        a->clk[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (threadIdx.x == 0) s_next_tile = kWaves;
+    auto at = [&](uint32_t x) { return x < b1 ? x : last; };   // the tile a load reads for claim x
+    auto claim = [&]() -> uint32_t {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(&s_next_tile, 1u);
+        return b0 + wave_uniform(c);
+    };
+    uint32_t g = b0 + wv;   // the wave's first tile (static), its loads in flight while the tables are written
+    BatchTile cb;
+    cb.hi = 0;
+    cb.j = ~0u;             // batch_map starts its search at batch 0
+    batch_map(a, at(g), cb);
+    RecWords cur = batch_load(cb, at(g), lane, inf_off, hf_off);
+    uint32_t g1 = 0;
+    BatchTile nb1 = cb;
+    RecWords r1 = cur;
+    if constexpr (DEPTH == 2) {
+        g1 = claim();
+        batch_map(a, at(g1), nb1);
+        r1 = batch_load(nb1, at(g1), lane, inf_off, hf_off);
+    }
+    fill_block<KEYSEL>(a->t0, a->tab, kBlock);
+    __syncthreads();
+    if (threadIdx.x == 0 && a->clk) a->clk[4 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const Lane l = lane_bases();
+    const bool keyok = KEYSEL != HFV_KEYSEL_ZERO || ukey.ok;   // slot 0 empty: fail closed (xdp.c:83-84)
+    // verdict words wait in a per-wave stash (lane k: the wave's k-th tile, with its own bitmap
+    // address, since a wave's tiles may belong to two batches) and go out as one scattered store
+    uint64_t st_word = 0, st_addr = 0;
+    uint32_t stashed = 0;
+    while (g < b1) {
+        const uint32_t ng = claim();
+        BatchTile nb = DEPTH == 2 ? nb1 : cb;
+        batch_map(a, at(ng), nb);
+        const RecWords rn = batch_load(nb, at(ng), lane, inf_off, hf_off);
+        const uint64_t rec = (uint64_t)(g - cb.lo) * 64 + lane;
+        uint64_t ballot = 0;
+        if (keyok) ballot = verify_tile<KEYSEL, true>(cur, rec < cb.n, l, &ukey);
+        if (lane == stashed) {
+            st_word = ballot;
+            st_addr = cb.bits + (uint64_t)(g - cb.lo) * 8;
+        }
+        if (++stashed == 64) {
+            *(GlobalU64 *)st_addr = st_word;
+            stashed = 0;
+        }
+        if constexpr (DEPTH == 2) {
+            cur = r1;
+            cb = nb1;
+            g = g1;
+            r1 = rn;
+            nb1 = nb;
+            g1 = ng;
+        } else {
+            cur = rn;
+            cb = nb;
+            g = ng;
+        }
+    }
+    if (lane < stashed) *(GlobalU64 *)st_addr = st_word;
+    if (lane == 0 && a->clk)   // the block's last wave to leave sets its finish stamp
+        __hip_atomic_fetch_max(&a->clk[4 + kBatchStampBlocks + blockIdx.x], __builtin_amdgcn_s_memrealtime(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a->clk) {
+        a->clk[2] = __builtin_amdgcn_s_memtime();
+        a->clk[3] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+int launch_verify_batches(const LaunchGeom &g, int keysel, const BatchArgs &args, void *stream, void *ev_start,
+                          void *ev_stop)
+{
+    auto k = keysel == HFV_KEYSEL_IFID ? k_verify_batches<HFV_KEYSEL_IFID, HFV_BATCH_DEPTH>
+                                       : k_verify_batches<HFV_KEYSEL_ZERO, HFV_BATCH_DEPTH>;
+    // one block per CU, but no more blocks than tiles: every block owns at least one tile
+    uint64_t blocks = args.total;
+    if (blocks > (uint64_t)g.num_cus) blocks = (uint64_t)g.num_cus;
+    hipExtLaunchKernelGGL(k, dim3((unsigned)(blocks ? blocks : 1)), dim3(kBlock), 0, (hipStream_t)stream,
+                          (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0u, args);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // resident verify service (hfv_service_*): one persistent 1024-thread block per CU verifies
 // batch after batch while the round tables (and the key image) stay in LDS
 // ---------------------------------------------------------------------------------------

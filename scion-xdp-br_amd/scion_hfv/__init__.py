@@ -69,6 +69,8 @@ def lib():
         "hfv_key_add_batch": (i32, [vp, u32, vp, sz]),
         "hfv_verify_records": (i32, [vp, vp, sz, sz, vp, vp]),
         "hfv_verify_records_timed": (i32, [vp, vp, sz, sz, vp, vp, ctypes.POINTER(ctypes.c_float)]),
+        "hfv_verify_batches": (i32, [vp, vp, sz, vp]),
+        "hfv_verify_batches_timed": (i32, [vp, vp, sz, vp, ctypes.POINTER(ctypes.c_float)]),
         "hfv_ctx_describe": (i32, [vp, ctypes.c_char_p, sz]),
         "hfv_ctx_attach_keymap": (i32, [vp, ctypes.c_char_p]),
         "hfv_keymap_path": (i32, [ctypes.c_char_p, ctypes.c_char_p, sz]),
@@ -385,6 +387,56 @@ class Ctx:
         ms = ctypes.c_float()
         _check(lib().hfv_verify_records_timed(self._h, _ptr(recs), stride, n, _ptr(pass_bits), _stream(stream),
                                               ctypes.byref(ms)))
+        return ms.value
+
+    def verify_batches(self, batches, stream=None):
+        """hfv_verify_batches: every batch of the list ([(recs, n, pass_bits[, stride]), ...] or a
+        service_batches array) in one stream-ordered launch (64 batches per launch)."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        _check(lib().hfv_verify_batches(self._h, arr, len(arr), _stream(stream)))
+
+    def verify_batches_fn(self, batches, stream=None):
+        """verify_batches as a prepared zero-argument call (one foreign-function call per use)."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        f, h, n, st = lib().hfv_verify_batches, self._h, len(arr), _stream(stream)
+
+        def run():
+            rc = f(h, arr, n, st)
+            if rc:
+                _check(rc)
+        return run
+
+    def batches_shader_mhz(self):
+        """Diagnostic: block 0's shader clock over the last verify_batches launch (s_memtime
+        against the 100 MHz s_memrealtime), or None."""
+        v = (ctypes.c_uint64 * 4)()
+        L = lib()
+        if not hasattr(L, "hfv_debug_batches_clock"):
+            return None
+        L.hfv_debug_batches_clock.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        if L.hfv_debug_batches_clock(self._h, v, 4) != 0:
+            return None
+        t0, r0, t1, r1 = (int(x) for x in v)
+        return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
+
+    def batches_block_span(self, grid):
+        """Diagnostic: per block of the last timed verify_batches launch, (fill done, finished) in
+        us after the earliest fill; None if unavailable."""
+        v = (ctypes.c_uint64 * (4 + 2 * 1024))()
+        L = lib()
+        L.hfv_debug_batches_clock.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        if L.hfv_debug_batches_clock(self._h, v, len(v)) != 0:
+            return None
+        st = [int(v[4 + k]) for k in range(grid)]
+        fin = [int(v[4 + 1024 + k]) for k in range(grid)]
+        t0 = min(st)
+        return [((a - t0) / 100.0, (b - t0) / 100.0) for a, b in zip(st, fin)]
+
+    def verify_batches_timed(self, batches, stream=None):
+        """verify_batches, waited for; returns the launches' execution time in ms."""
+        arr = batches if isinstance(batches, ctypes.Array) else self.service_batches(batches)
+        ms = ctypes.c_float(0.0)
+        _check(lib().hfv_verify_batches_timed(self._h, arr, len(arr), _stream(stream), ctypes.byref(ms)))
         return ms.value
 
     def verdict_counters(self, recs, n, pass_bits, counters, stride=REC_SIZE, stream=None):

@@ -33,8 +33,10 @@ def main():
                 sys.exit(1)
             d = json.loads(line[0])
             s = d["service"] or {}
+            b = d.get("batches") or {}
             print(f"{r} {os.path.basename(lib) + ('@' + envs if envs else ''):32s} value {d['value']:9.1f} grid_ms {s.get('grid_ms')} "
-                  f"mhz {s.get('shader_mhz')} launch {d['per_launch']['mpkts']:9.1f} "
+                  f"mhz {s.get('shader_mhz')} batches_ms {b.get('kernel_ms')} {b.get('kernel_ms_all')} mhz {b.get('shader_mhz')} "
+                  f"launch {d['per_launch']['mpkts']:9.1f} "
                   f"launch_kernel_us {d['per_launch']['kernel_ms_mean'] * 1e3:6.2f}", flush=True)
 
 

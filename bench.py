@@ -15,19 +15,23 @@ report).  The rank's records sit in R distinct resident batches (default R = 8: 
 reads its records from HBM, not from the memory-side cache; every step writes its own
 verdict bitmap.
 
-By default (--mode service) the K steps are K batches posted to the resident service
-(hfv_service_submitv: the XDP program's counterpart, a grid that stays on the GPU), with the
-grid launch, its table fill and its drain inside the timed region; --mode launch times one
-hfv_verify_records launch per step instead (both are always measured: `service`,
-`per_launch`).  Rank 0 prints one JSON line.  Besides the contract fields it carries:
+By default (--mode batches) the K steps are K batches verified by ONE stream-ordered
+hfv_verify_batches call on the rank's stream (one launch per 64 batches: the AES tables are
+written into LDS once, the batches' tiles dealt to the CUs as one contiguous range), the launch
+and its table fill inside the timed region; --mode service posts the K batches to the resident
+service (hfv_service_run_async: a persistent grid fed through a host descriptor ring) and
+--mode launch times one hfv_verify_records launch per step (all three are always measured:
+`batches`, `service`, `per_launch`).  Rank 0 prints one JSON line.  Besides the contract
+fields it carries:
   roofline      -- the headline kernel's algorithmic bytes (64 B read + 1/8 B verdict per
                    record) / its duration from the dispatch's own start/stop events (the
-                   service grid's lifetime over all K batches), against the 8 TB/s HBM3E
-                   peak; `traffic` is the PMC-measured HBM bytes per batch of the same
-                   configuration (profiles/traffic.json), when one was measured.
+                   launch's, or the service grid's lifetime, over all K batches), against the
+                   8 TB/s HBM3E peak and against a streaming read of the same resident batches
+                   timed in the same run (`achievable_peak`); `traffic` is the PMC-measured HBM
+                   bytes per batch of the same configuration (profiles/traffic.json).
   ceilings      -- LDS lookups and VALU instructions per packet read at run time from the
                    committed PMC summary of this configuration, and the LDS-issue bound at
-                   the shader clock the grid ran at.
+                   the shader clock the timed kernel ran at (block 0's s_memtime).
   cpu_baseline  -- the reference's own aes.c soft path (oracle/_ref, built from
                    /root/reference) over the same records on this host's cores (median of
                    >= 5 timed passes), verdicts cross-checked against the GPU bitmap; 1-core
@@ -76,11 +80,14 @@ SEED_RECORDS = 0x5C100001
 SEED_KEYS = 0x5C100100
 KEY_1111 = b"1111111111111111"   # br/test/run_tests:113
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-HBM_ACHIEVABLE_GBS = 6500.0      # a pure streaming read of the records' access pattern (scripts/ubench/stream_read.hip: 6.4-6.6 TB/s)
 BYTES_PER_PACKET = 64 + 1.0 / 8  # algorithmic bytes per verified record
 M64 = (1 << 64) - 1
 # committed PMC summary of the headline configuration (scripts/pmc_round.sh ... svc rot)
-PMC_SUMMARY = {"zero": "profiles/r05/final/pmc_zero_svc/summary.json", "ifid": "profiles/r05/pmc_ifid_svc/summary.json"}
+# committed PMC summaries of the headline configurations, by (keysel, path)
+PMC_SUMMARY = {("zero", "service"): "profiles/r05/final/pmc_zero_svc/summary.json",
+               ("ifid", "service"): "profiles/r05/pmc_ifid_svc/summary.json",
+               ("zero", "batches"): "profiles/r06/pmc_zero_bat/summary.json",
+               ("ifid", "batches"): "profiles/r06/pmc_ifid_bat/summary.json"}
 METRIC = "Mpkt/s device-resident hop-field AES-CMAC verify, 64 B SCION packets"
 
 
@@ -205,6 +212,14 @@ class World:
         self.dist.all_gather(out, t)
         return [float(o.item()) for o in out]
 
+    def gather_obj(self, x):
+        """Every rank's picklable x (rank order) on every rank."""
+        if self.size == 1:
+            return [x]
+        out = [None] * self.size
+        self.dist.all_gather_object(out, x)
+        return out
+
     def timed(self, steps, fn):
         """fn() `steps` times between barrier + device sync on both sides; (max over ranks,
         per-rank list).  Each rank's clock runs from the release of the opening barrier to the
@@ -275,10 +290,10 @@ def make_ctx(hfv, device, keysel):
     return ctx
 
 
-def pmc_summary(keysel):
-    """The committed PMC summary of the headline configuration for this keysel, or None."""
+def pmc_summary(keysel, path="batches"):
+    """The committed PMC summary of the headline configuration for this keysel and path, or None."""
     try:
-        return json.load(open(os.path.join(ROOT, PMC_SUMMARY[keysel])))
+        return json.load(open(os.path.join(ROOT, PMC_SUMMARY[(keysel, path)])))
     except Exception:
         return None
 
@@ -304,13 +319,13 @@ def settle(args):
 LOOKUPS_PER_PKT = 145   # T-table lookups per packet (11 + 8 x 16 + 6), each addressed by one v_perm
 
 
-def ceilings(keysel, n, mhz, cus):
+def ceilings(keysel, n, mhz, cus, path="batches"):
     """Bounds beside HBM, per packet, read from the committed PMC summary of this
     configuration (SQ_INSTS_LDS / SQ_INSTS_VALU are wave-instructions: x 64 lanes / records
     per batch) and the chip's conflict-free ds_read_b32 issue rate (32 lanes per clock per
     CU, MI355X_MICROARCH.md LDS table) at the shader clock the grid ran at."""
-    s = pmc_summary(keysel)
-    out = {"source": PMC_SUMMARY[keysel] if s else None}
+    s = pmc_summary(keysel, path)
+    out = {"source": PMC_SUMMARY[(keysel, path)] if s else None}
     row = (s or {}).get(str(n))
     if not row:
         return out
@@ -385,7 +400,7 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         b.zero_()
     run_b()
     W.sync()
-    check(max(R, steps))
+    check(steps)
     b_runs = []
     for _ in range(max(1, reps)):
         for b in bitmaps:
@@ -399,6 +414,16 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         b_ms.append((ctx.verify_batches_timed(blist, stream=stream), ctx.batches_shader_mhz()))
     check(steps)
     b_med = sorted(b_ms)[len(b_ms) // 2]
+    # the achievable HBM read rate of these same resident batches in this run: one dense
+    # non-temporal streaming read over the K batches (the rotation the steps read), 4 blocks per CU
+    sr = sorted(ctx.stream_read_ms([batches[k % R] for k in range(min(steps, 64))], stream=stream)
+                for _ in range(max(3, reps)))
+    sr_bytes = min(steps, 64) * n * 64
+    out["stream_read"] = {"gbs": round(sr_bytes / (sr[len(sr) // 2] * 1e-3) / 1e9, 1),
+                          "gbs_best": round(sr_bytes / (sr[0] * 1e-3) / 1e9, 1),
+                          "ms_all": [round(x, 4) for x in sr], "bytes": sr_bytes,
+                          "kernel": "k_stream_read: 16 B non-temporal loads per lane, 4 x 1024-thread blocks per CU, "
+                                    "over the same resident batches (hfv_debug_stream_read)"}
     out.update({"bat_el": b_runs[len(b_runs) // 2][0], "bat_per_rank_s": b_runs[len(b_runs) // 2][1],
                 "bat_all_ms": [round(r[0] * 1e3, 4) for r in b_runs], "bat_kernel_ms": b_med[0],
                 "bat_mhz": b_med[1], "bat_all_kernel_ms": [round(x[0], 4) for x in b_ms],
@@ -467,8 +492,10 @@ def measure_hf(hfv, W, ctx, keysel_name, n, first, rotate, steps, warmup, stream
         runs = truns
     runs.sort(key=lambda r: r[0])
     truns_s = sorted(truns, key=lambda r: r[2])
-    svc_el, per_rank, _, mhz = runs[len(runs) // 2][:4]
-    grid_ms = truns_s[len(truns_s) // 2][2]
+    svc_el, per_rank = runs[len(runs) // 2][:2]
+    # the roofline's grid and ITS shader clock (the ceilings are priced at the clock of the grid
+    # the roofline times)
+    grid_ms, mhz = truns_s[len(truns_s) // 2][2], truns_s[len(truns_s) // 2][3]
     out.update({"svc_el": svc_el, "per_rank_s": per_rank, "grid_ms": grid_ms, "mhz": mhz,
                 "svc_all_ms": [round(r[0] * 1e3, 4) for r in runs],
                 "svc_all_call_us": [round(r[4], 1) for r in runs],
@@ -883,7 +910,7 @@ def host_leg(hfv, W, ctx, recs, n, ref_bits):
                                            "whole 64 B lines), bitmap written to registered host memory"}}
 
 
-def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, inflight=2, dma=2):
+def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, inflight=2, dma=2, digest=False):
     """Config 5 in one process (hfv_loop_run): gen_packets.py's 1000 frames cycled by producer
     threads into a pinned RX ring, the router (br1-ff00_0_1-2 of br/evaluation) over each chunk
     (dma: 0 zero-copy, 1 through HBM both ways, 2 copied in and the changes written back by the
@@ -894,7 +921,7 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
     frames = E.frames(1000)
     lens = np.full(1000, E.FRAME_LEN, dtype=np.uint16)
     kw = dict(rx_ifindex=E.RX_IFINDEX, slot=slot, chunk=chunk, chunks=chunks, producers=producers,
-              consumers=consumers, inflight=inflight, dma=dma)
+              consumers=consumers, inflight=inflight, dma=dma, digest=digest)
     ctx.loop_run(frames, lens, 4 * chunk, **kw)                          # warm up
     W.barrier()
     # a failure on one rank must not leave the others waiting in the gather: every rank gets
@@ -908,8 +935,17 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
     times = W.gather(r["seconds"] if r and not err else -1.0)
     ctx_numa = ctx.numa_node()
     ctx.close()
+    # every rank's counts (and, with digest, the order-free digest of its transmitted frames) and
+    # where its producer / consumer threads ran
+    mine = {"rank": W.rank, "error": err}
+    if r:
+        mine.update({k: r[k] for k in ("rx", "tx", "tx_bytes", "drop", "verdicts", "numa_node", "threads",
+                                        "threads_on_node")})
+        mine["tx_digest"] = f"{r['tx_digest']:016x}" if digest else None
+        mine["seconds"] = round(r["seconds"], 4)
+    per_rank = W.gather_obj(mine)
     if min(times) < 0:
-        return {"error": err or "a rank's loop failed", "per_rank_s": times}
+        return {"error": err or "a rank's loop failed", "per_rank_s": times, "per_rank": per_rank}
     el = max(times)
     r["numa_node"] = ctx_numa
     return {"mpkts": round(W.size * total / el / 1e6, 2), "seconds": round(el, 4), "frames_per_gpu": total,
@@ -917,6 +953,7 @@ def measure_loop(hfv, W, total, chunk, chunks, producers, consumers, slot=144, i
             "inflight": inflight, "router_io": ("zero-copy over PCIe", "DMA through HBM both ways",
                           "DMA in, changed bytes written back by the kernel")[int(dma)],
             "tx_gbit_s": round(W.size * total * E.FRAME_LEN * 8 / el / 1e9, 1), "numa_node": r.get("numa_node"),
+            "per_rank": per_rank,
             "stage_busy_frac": {"router": round(r["gpu_busy_s"] / r["seconds"], 3),
                                 "router_waiting_for_rx": round(r["gpu_wait_s"] / r["seconds"], 3),
                                 "producer": round(r["producer_busy_s"] / producers / r["seconds"], 3),
@@ -935,7 +972,7 @@ def run_loop(args, W):
     tb = apply_thread_budget(args, thread_budget(W, c))
     c.close()
     r = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads, args.loop_consumers,
-                     args.loop_slot, args.loop_inflight, args.loop_dma)
+                     args.loop_slot, args.loop_inflight, args.loop_dma, args.loop_digest)
     result = {
         "metric": "Mpkt/s config-5 loop: RX ring -> border router on the GPU -> TX/drop, 138 B frames",
         "value": r.get("mpkts"), "unit": "Mpkt/s", "n_gpus": W.n_gpus, "ranks": W.size, "steps": 1, "warmup": 1,
@@ -990,7 +1027,7 @@ def run_hf(args, W):
     # an extra leg (host threads, PCIe copies) while another is still in its headline regions
     per_rank_grid = W.gather(m["grid_ms"] or 0.0)
     W.barrier()
-    headline = "launch" if args.launch_only and args.mode == "service" else args.mode
+    headline = "launch" if args.launch_only else args.mode
     elapsed = {"service": m["svc_el"], "launch": m["launch_el"], "batches": m["bat_el"]}[headline]
     if headline == "batches":
         m["per_rank_s"] = m["bat_per_rank_s"]
@@ -1039,12 +1076,16 @@ def run_hf(args, W):
                    "parallelism": f"batch-sharded x{W.size}, no collective"},
         "roofline": dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}, **kern,
-                         achievable_peak=HBM_ACHIEVABLE_GBS,
-                         frac_of_achievable=round(achieved / HBM_ACHIEVABLE_GBS, 4),
+                         achievable_peak=m["stream_read"]["gbs"],
+                         frac_of_achievable=round(achieved / m["stream_read"]["gbs"], 4),
+                         achievable_source="median of a dense streaming read of the same resident batches in this "
+                                           "run (stream_read)",
                          variant=ctx.describe(),
                          note=f"step k verifies resident batch k % {args.rotate} ({args.rotate} x {n * 64 >> 20} MiB "
                               f"per GPU > 256 MiB Infinity Cache): records are read from HBM"),
-        "ceilings": ceilings(args.keysel, n, m["bat_mhz"] if headline == "batches" else m["mhz"], cus),
+        "stream_read": m["stream_read"],
+        "ceilings": ceilings(args.keysel, n, m["bat_mhz"] if headline == "batches" else m["mhz"], cus,
+                             "batches" if headline == "batches" else "service"),
         "path": {"service": "resident service: one persistent grid; the K batches and a stop descriptor posted "
                             "through the host descriptor ring by one hfv_service_run_async call, which launches the "
                             "grid after them; the timed region's closing device synchronize waits for the grid to "
@@ -1148,7 +1189,11 @@ def run_hf(args, W):
                              "grids_ms": m3["svc_all_grid_ms"], "grids_mhz": m3["svc_grid_mhz"],
                              "per_launch_mpkts": round(total * args.steps / m3["launch_el"] / 1e6, 2),
                              "shader_mhz": round(m3["mhz"], 1) if m3["mhz"] else None,
-                             "ceilings": ceilings("ifid", n, m3["mhz"], cus)}
+                             "batches_kernel_ms": round(m3["bat_kernel_ms"], 4),
+                             "batches_frac": round(bytes_per_batch * args.steps / (m3["bat_kernel_ms"] * 1e-3) / 1e9
+                                                   / HBM_PEAK_GBS, 4),
+                             "batches_mpkts": round(total * args.steps / m3["bat_el"] / 1e6, 2),
+                             "ceilings": ceilings("ifid", n, m3["mhz"], cus, "service")}
         del m3
         ctx3.close()
 
@@ -1177,7 +1222,8 @@ def run_hf(args, W):
     if args.loop_n and not args.no_extras:   # config 5 runs on every rank (8x batch-sharded at N = 8)
         W.sync()
         result["config5_loop"] = measure_loop(hfv, W, args.loop_n, args.loop_chunk, args.loop_chunks, args.loop_threads,
-                                              args.loop_consumers, args.loop_slot, args.loop_inflight, args.loop_dma)
+                                              args.loop_consumers, args.loop_slot, args.loop_inflight, args.loop_dma,
+                                              args.loop_digest)
 
     if extras:
         result["settle_s_before_extra_legs"] = args.settle_s
@@ -1223,9 +1269,11 @@ def main():
     ap.add_argument("--loop-dma", type=int, default=2, choices=(0, 1, 2),
                     help="config-5 loop router I/O: 0 zero-copy over PCIe, 1 DMA through HBM both ways, "
                          "2 DMA in + the kernel writing its changes into the ring")
-    ap.add_argument("--mode", choices=["service", "launch", "batches"], default="service",
-                    help="hf headline: resident service grid (default), one launch per batch, or the K batches "
-                         "in one stream-ordered hfv_verify_batches call")
+    ap.add_argument("--loop-digest", action="store_true",
+                    help="config-5 loop: consumers sum a 64-bit digest of every transmitted frame (per rank in the line)")
+    ap.add_argument("--mode", choices=["service", "launch", "batches"], default="batches",
+                    help="hf headline: the K batches in one stream-ordered hfv_verify_batches call (default), "
+                         "the resident service grid, or one launch per batch")
     ap.add_argument("--settle-s", type=float, default=0.5, help="idle seconds before each extra leg (untimed)")
     ap.add_argument("--svc-reps", type=int, default=5, help="timed service regions of K steps (median reported; 5: robust to two host hiccups)")
     ap.add_argument("--launch-only", action="store_true",

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HFV_ABI_VERSION 2
+#define HFV_ABI_VERSION 3
 #define HFV_MAX_KEYS 256          /* key slots; the reference map holds 8 (maps.h:60-67) */
 #define HFV_REC_INF_OFF 40        /* default 64 B record layout, DESIGN.md section 3 */
 #define HFV_REC_HF_OFF 48
@@ -495,6 +495,10 @@ struct hfv_loop_stats {
     double producer_busy_s, consumer_busy_s;    /* summed over the threads of each side */
     uint64_t rx_truncated, tx_errors;           /* packet I/O: frames longer than a slot (dropped),
                                                    sends that failed after retries */
+    int32_t numa_node;                          /* the GPU's NUMA node the threads were pinned to (-1: unknown) */
+    uint32_t threads;                           /* producer + consumer threads */
+    uint32_t threads_on_node;                   /* ... of which ended their work on a CPU of that node */
+    uint32_t pad_;
 };
 int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *cfg, struct hfv_loop_stats *out);
 

@@ -286,14 +286,48 @@ static bool own_stream(const hfv_ctx *ctx, hipStream_t st);
 #define HFV_PUB_FENCE 1
 #endif
 
-// Test-only (hfv_debug_publish_delay): every publish copy waits behind a spin of this many
-// microseconds on its stream, so a test can make the cross-stream race deterministic.
+// Test hooks.  They change what the library does (delays, launch shapes) and exist only in the
+// test build, lib/libscionhfv_test.so (make: -DHFV_TEST_HOOKS); the product library has none of
+// them (tests/test_abi.py checks the exports).  The GPU tests that need one run in a child process
+// on the test build (tests/conftest.py: rerun_on_test_build).
+#ifdef HFV_TEST_HOOKS
+// hfv_debug_publish_delay: every publish copy waits behind a spin of this many microseconds on
+// its stream, so a test can make the cross-stream race deterministic.
 static uint32_t g_pub_delay_us = 0;
 extern "C" int hfv_debug_publish_delay(uint32_t us)
 {
     g_pub_delay_us = us;
     return 0;
 }
+// hfv_debug_br_grid: blocks per k_br_process launch (0 = one block per CU up to the tile count).
+// With 1, a 1000-frame chunk runs as 16 active waves of one block -- the shape the round-2 loop
+// failure ran in ("loop parity failure").
+static unsigned g_br_grid = 0;
+extern "C" int hfv_debug_br_grid(unsigned blocks)
+{
+    g_br_grid = blocks;
+    return 0;
+}
+// hfv_debug_br_split: split launches that count verdicts into pieces of at most `frames` frames
+// (0 = only where 32-bit block counters could overflow), so a test can check that split launches
+// add up to the same counters and outputs.
+static size_t g_br_split = 0;
+extern "C" int hfv_debug_br_split(size_t frames)
+{
+    g_br_split = frames;
+    return 0;
+}
+static LaunchGeom br_geom(const hfv_ctx *ctx)
+{
+    LaunchGeom g = ctx->geom;
+    g.br_grid_cap = g_br_grid;
+    g.br_split_cap = g_br_split;
+    return g;
+}
+#else
+static constexpr uint32_t g_pub_delay_us = 0;
+#define br_geom(ctx) ((ctx)->geom)
+#endif
 
 // Make the shadow table visible to work enqueued next on `st` -- and, once the copy is queued,
 // to work on any other stream (which waits for the copy until it has been seen complete);
@@ -798,6 +832,34 @@ extern "C" int hfv_debug_batches_clock(hfv_ctx *ctx, uint64_t *out, size_t words
     return 0;
 }
 
+// Diagnostic (not part of include/scion_hfv.h): one dense non-temporal streaming read of `count`
+// (<= 64) device buffers on `stream`, waited for; *kernel_ms = its dispatch time.  bench.py prices
+// the verify kernel against this rate over the same resident batches (roofline.achievable_peak).
+extern "C" int hfv_debug_stream_read(hfv_ctx *ctx, const void *const *bufs, const size_t *bytes, size_t count,
+                                     void *stream, float *kernel_ms)
+{
+    if (!ctx || !bufs || !bytes || !kernel_ms || count == 0 || count > kBatchMax) return fail(-EINVAL, "bad argument");
+    DeviceGuard g(ctx->device);
+    SVC_QUIESCE(ctx);
+    for (int i = 0; i < 2; ++i)
+        if (!ctx->tev[i]) HIP_TRY(hipEventCreate(&ctx->tev[i]));
+    StreamArgs a;
+    memset(&a, 0, sizeof a);
+    a.nb = (uint32_t)count;
+    a.sink = (uint32_t *)ctx->bat_clk;   // never written in practice (see k_stream_read)
+    for (size_t i = 0; i < count; ++i) {
+        if (((uintptr_t)bufs[i] & 15) || (bytes[i] & 15)) return fail(-EINVAL, "buffer %zu not 16-byte aligned", i);
+        a.buf[i] = bufs[i];
+        a.bytes[i] = bytes[i];
+    }
+    hipStream_t st = pick_stream(ctx, stream);
+    int e = launch_stream_read(ctx->geom, a, st, ctx->tev[0], ctx->tev[1]);
+    if (e != hipSuccess) return hip_fail((hipError_t)e, "stream read launch");
+    HIP_TRY(hipEventSynchronize(ctx->tev[1]));
+    HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
 // Diagnostic (not part of include/scion_hfv.h): the default KEYSEL_ZERO kernel with per-wave
 // s_memrealtime stamps, for the timeline analysis in scripts/stamps.py.  stamps: device
 // buffer of (grid * 16 waves) x 16 u64; returns the grid size in *grid.
@@ -1002,7 +1064,7 @@ int hfv_br_process(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_t *len
     DevState *ds;
     rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
+    int e = launch_br_process(br_geom(ctx), ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
                               action, verdict, egress_ifindex, stats, st);
     return after_launch(ctx, st, e, "br_process launch");
 }
@@ -1025,7 +1087,7 @@ int hfv_br_process_timed(hfv_ctx *ctx, uint8_t *pkts, size_t slot, const uint16_
     DevState *ds;
     rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
+    int e = launch_br_process(br_geom(ctx), ds, pkts, slot, (uint32_t)slot, (uint32_t)slot, len, ingress_ifindex, n,
                               action, verdict, egress_ifindex, stats, st, ctx->tev[0], ctx->tev[1]);
     rc = after_launch(ctx, st, e, "br_process launch");
     if (rc) return rc;
@@ -1272,7 +1334,7 @@ static int brh_chunk(hfv_ctx *ctx, int sl, uint8_t *frames, size_t fstride, size
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, ctx->brh_dwin[sl], window, (uint32_t)maxlen, (uint32_t)window,
+    int e = launch_br_process(br_geom(ctx), ds, ctx->brh_dwin[sl], window, (uint32_t)maxlen, (uint32_t)window,
                               (const uint16_t *)dio, (const uint32_t *)(dio + kBrChunk * 2), cnt,
                               dio + kBrChunk * 6, dio + kBrChunk * 7, (int32_t *)(dio + kBrChunk * 8),
                               ctx->brh_dstats, st);
@@ -1337,7 +1399,7 @@ static int br_zero_copy(hfv_ctx *ctx, uint8_t *dframes, size_t slot, const uint1
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
+    int e = launch_br_process(br_geom(ctx), ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
                               degr, ctx->brh_dstats, st);
     rc = after_launch(ctx, st, e, "br_process launch");
     if (rc) return rc;
@@ -1386,7 +1448,7 @@ int hfv::br_dev_launch(hfv_ctx *ctx, void *stream, uint8_t *dframes, size_t slot
     DevState *ds;
     int rc = publish_keys(ctx, st, &ds);
     if (rc) return rc;
-    int e = launch_br_process(ctx->geom, ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
+    int e = launch_br_process(br_geom(ctx), ds, dframes, slot, (uint32_t)slot, (uint32_t)slot, dlen, difx, n, dact, dver,
                               degr, dstats, st, nullptr, nullptr, dout);
     return after_launch(ctx, st, e, "br_process launch");
 }
@@ -1885,7 +1947,11 @@ static int svc_begin(hfv_ctx *ctx, uint32_t idle_ms, DevState **ds)
     return 0;
 }
 
+#ifdef HFV_TEST_HOOKS
 static uint32_t g_svc_relay_delay_us = 0;   // hfv_debug_relay_delay
+#else
+static constexpr uint32_t g_svc_relay_delay_us = 0;
+#endif
 
 static inline uint64_t mono_ns()
 {
@@ -2255,13 +2321,15 @@ int hfv_debug_service_call_ns(hfv_ctx *ctx, uint64_t out[5])
     return 0;
 }
 
-// Test hook (not part of include/scion_hfv.h): every host read of later service grids' relay
-// wave takes `us` microseconds longer (a slow PCIe link), 0 = off.
+#ifdef HFV_TEST_HOOKS
+// Test hook (test build only): every host read of later service grids' relay wave takes `us`
+// microseconds longer (a slow PCIe link), 0 = off.
 int hfv_debug_relay_delay(uint32_t us)
 {
     g_svc_relay_delay_us = us > 100000u ? 100000u : us;
     return 0;
 }
+#endif
 
 // ---- memory helpers -------------------------------------------------------------------
 

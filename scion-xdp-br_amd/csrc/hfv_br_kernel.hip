@@ -1001,25 +1001,6 @@ extern "C" int hfv_debug_br_prof(unsigned long long out[8])
 }
 #endif
 
-// Test-only launch-geometry override (hfv_debug_br_grid): blocks per k_br_process launch, 0 =
-// one block per CU up to the tile count.  With 1, a 1000-frame chunk runs as 16 active waves of
-// one block -- the shape the round-2 loop failure ran in ("loop parity failure").
-static unsigned g_br_grid_override = 0;
-extern "C" int hfv_debug_br_grid(unsigned blocks)
-{
-    g_br_grid_override = blocks;
-    return 0;
-}
-// Test-only (hfv_debug_br_split): split launches that count verdicts into pieces of at most
-// `frames` frames (0 = only where 32-bit block counters could overflow), so a test can check
-// that split launches add up to the same counters and outputs.
-static size_t g_br_split_override = 0;
-extern "C" int hfv_debug_br_split(size_t frames)
-{
-    g_br_split_override = frames;
-    return 0;
-}
-
 int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, size_t slot, uint32_t maxlen,
                       uint32_t window, const uint16_t *len, const uint32_t *ingress_ifindex, size_t n,
                       uint8_t *action, uint8_t *verdict, int32_t *egress_ifindex, uint64_t *stats, void *stream,
@@ -1055,7 +1036,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
         // a block's range is ceil(tiles / grid) tiles at most, i.e. up to a tile more than the even
         // share plus a tile of rounding: reserve two tiles
         uint64_t cap_n = (per_block > 128 ? per_block - 128 : 1) * (uint64_t)g.num_cus;
-        if (g_br_split_override && g_br_split_override < cap_n) cap_n = g_br_split_override;
+        if (g.br_split_cap && g.br_split_cap < cap_n) cap_n = g.br_split_cap;   // test build only
         if ((uint64_t)n > cap_n) {
             for (size_t off = 0; off < n; off += cap_n) {
                 const size_t m = n - off < cap_n ? n - off : (size_t)cap_n;
@@ -1071,7 +1052,7 @@ int launch_br_process(const LaunchGeom &g, const DevState *st, uint8_t *pkts, si
 #endif
     const uint64_t tiles = (n + 63) / 64, cap = (uint64_t)g.num_cus;   // one block per CU at most
     unsigned grid = (unsigned)(tiles < cap ? (tiles ? tiles : 1) : cap);
-    if (g_br_grid_override && g_br_grid_override < grid) grid = g_br_grid_override;
+    if (g.br_grid_cap && g.br_grid_cap < grid) grid = g.br_grid_cap;   // test build only
     hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
                           (hipEvent_t)ev_stop, 0u, st, (const uint8_t *)pkts, out, (uint64_t)slot, maxlen,
                           window, len, ingress_ifindex, (uint64_t)n, action, verdict, egress_ifindex,

@@ -170,6 +170,10 @@ constexpr uint64_t kSvcWatchdog = 3;    // a wave gave up waiting for its block'
 struct LaunchGeom {
     int num_cus;
     int svc_blocks;   // blocks of a service grid: num_cus, or fewer (hfv_service_set_grid)
+    // test-only overrides of the router launch (the test build's hfv_debug_br_grid / br_split;
+    // always 0 in the product library): blocks per k_br_process launch, frames per split launch
+    unsigned br_grid_cap = 0;
+    uint64_t br_split_cap = 0;
 };
 
 // kernel launchers (hfv_kernels.hip); return hipError_t as int
@@ -281,6 +285,14 @@ struct BatchArgs {
 static_assert(sizeof(BatchArgs) <= 4096, "BatchArgs exceeds the 4 KiB kernel-argument segment");
 int launch_verify_batches(const LaunchGeom &g, int keysel, const BatchArgs &args, void *stream, void *ev_start,
                           void *ev_stop);
+// diagnostic streaming read (hfv_debug_stream_read): nb device buffers, read densely
+struct StreamArgs {
+    uint32_t nb, pad_;
+    uint32_t *sink;
+    const void *buf[kBatchMax];
+    uint64_t bytes[kBatchMax];
+};
+int launch_stream_read(const LaunchGeom &g, const StreamArgs &args, void *stream, void *ev_start, void *ev_stop);
 // full border-router path (hfv_br_kernel.hip)
 // slot: bytes between frames in `pkts`; maxlen: lengths are clamped to it (the caller's
 // slot); window: bytes of each frame present (frames needing more get HFV_BR_ACTION_RETRY).

@@ -292,6 +292,10 @@ __device__ __forceinline__ RecWords batch_load(const BatchTile &b, uint32_t g, u
 #ifndef HFV_BATCH_DEPTH
 #define HFV_BATCH_DEPTH 1
 #endif
+// HFV_BATCH_PIN: each AES round's issue order pinned (16 addresses, 16 reads, 8 xor3; round_full)
+#ifndef HFV_BATCH_PIN
+#define HFV_BATCH_PIN 1
+#endif
 template <int KEYSEL, int DEPTH>
 __global__ __launch_bounds__(kBlock) void k_verify_batches(const BatchArgs args)
 {
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_verify_batches(const BatchArgs args)
         const RecWords rn = batch_load(nb, at(ng), lane, inf_off, hf_off);
         const uint64_t rec = (uint64_t)(g - cb.lo) * 64 + lane;
         uint64_t ballot = 0;
-        if (keyok) ballot = verify_tile<KEYSEL, true>(cur, rec < cb.n, l, &ukey);
+        if (keyok) ballot = verify_tile<KEYSEL, HFV_BATCH_PIN != 0>(cur, rec < cb.n, l, &ukey);
         if (lane == stashed) {
             st_word = ballot;
             st_addr = cb.bits + (uint64_t)(g - cb.lo) * 8;
@@ -389,6 +393,35 @@ int launch_verify_batches(const LaunchGeom &g, int keysel, const BatchArgs &args
     uint64_t blocks = args.total;
     if (blocks > (uint64_t)g.num_cus) blocks = (uint64_t)g.num_cus;
     hipExtLaunchKernelGGL(k, dim3((unsigned)(blocks ? blocks : 1)), dim3(kBlock), 0, (hipStream_t)stream,
+                          (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0u, args);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// diagnostic: the HBM streaming-read rate of a list of device buffers (hfv_debug_stream_read),
+// the achievable peak a bench run prices its verify kernel against -- the same resident batches,
+// read densely (16 B per lane per load, non-temporal), 4 blocks of 1024 threads per CU
+// (scripts/ubench/stream_read.hip: 7.05 TB/s on a 1 GiB buffer, round 1)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_stream_read(const StreamArgs args)
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t acc = 0;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t j = 0; j < args.nb; ++j) {
+        const u32x4 *p = (const u32x4 *)args.buf[j];
+        const uint64_t n = args.bytes[j] / 16;
+        for (uint64_t i = tid; i < n; i += nthr) {
+            const u32x4 v = __builtin_nontemporal_load(p + i);
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9e3779b9u) args.sink[0] = acc;   // keeps the loads; never true for the bench's records in practice
+}
+
+int launch_stream_read(const LaunchGeom &g, const StreamArgs &args, void *stream, void *ev_start, void *ev_stop)
+{
+    hipExtLaunchKernelGGL(k_stream_read, dim3(4 * g.num_cus), dim3(1024), 0, (hipStream_t)stream,
                           (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0u, args);
     return (int)hipGetLastError();
 }

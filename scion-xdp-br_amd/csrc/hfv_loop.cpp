@@ -71,16 +71,18 @@ static double now_s()
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
-static void pin(int numa_node)
+// Pin the calling thread to the CPUs of `numa_node` it may use; returns that set (empty when the
+// node is unknown or none of its CPUs is allowed: the thread then stays where it was).
+static cpu_set_t pin(int numa_node)
 {
-    if (numa_node < 0) return;
+    cpu_set_t allowed, cpus;
+    CPU_ZERO(&cpus);
+    if (numa_node < 0) return cpus;
     char path[128];
     snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", numa_node);
     FILE *f = fopen(path, "r");
-    if (!f) return;
-    cpu_set_t allowed, cpus;
-    CPU_ZERO(&cpus);
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) { fclose(f); return; }
+    if (!f) return cpus;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) { fclose(f); return cpus; }
     int a, b;
     char sep = 0;
     while (fscanf(f, "%d", &a) == 1) {
@@ -95,6 +97,14 @@ static void pin(int numa_node)
     }
     fclose(f);
     if (CPU_COUNT(&cpus) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus, &cpus);
+    return cpus;
+}
+
+// The thread runs on a CPU of `cpus` now (checked where a thread ends its work).
+static bool on_node(const cpu_set_t &cpus)
+{
+    const int cpu = sched_getcpu();
+    return CPU_COUNT(&cpus) > 0 && cpu >= 0 && CPU_ISSET(cpu, &cpus);
 }
 
 // ---- packet sockets (the evaluation's veth ends) ---------------------------------------------
@@ -144,23 +154,32 @@ struct Chunk {
     size_t n = 0;                     // frames in it
 };
 
-// Test-only router stage on the host (hfv_debug_loop_host_stage): with it set, hfv_loop_run
-// takes no ctx, keeps the ring in ordinary memory and calls the function on each filled chunk
-// in place of the kernel, so the ring, the threads and the packet-socket I/O run on a machine
-// without a GPU (tests/test_loop_pktio.py drives them over veth pairs with the oracle router).
+// Test-only router stage on the host (hfv_debug_loop_host_stage, in the test build
+// lib/libscionhfv_test.so only): with it set, hfv_loop_run takes no ctx, keeps the ring in
+// ordinary memory and calls the function on each filled chunk in place of the kernel, so the
+// ring, the threads and the packet-socket I/O run on a machine without a GPU
+// (tests/test_loop_pktio.py drives them over veth pairs with the oracle router).  The product
+// library has no such seam: its router stage is always the kernel.
+#ifdef HFV_TEST_HOOKS
 static hfv::hfv_loop_host_stage_fn g_host_stage = nullptr;
 static void *g_host_stage_user = nullptr;
+#else
+static constexpr hfv::hfv_loop_host_stage_fn g_host_stage = nullptr;
+static constexpr void *g_host_stage_user = nullptr;
+#endif
 
 }  // namespace
 
 using namespace hfv;
 
+#ifdef HFV_TEST_HOOKS
 extern "C" int hfv_debug_loop_host_stage(hfv::hfv_loop_host_stage_fn fn, void *user)
 {
     g_host_stage = fn;
     g_host_stage_user = user;
     return 0;
 }
+#endif
 
 extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struct hfv_loop_stats *out)
 {
@@ -312,8 +331,14 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
 
     // producers: chunk k by producer k % P (tcpreplay --loop of the frame list)
     std::vector<double> busy(producers, 0.0);
+    std::atomic<uint32_t> threads_on_node{0};
     auto produce = [&](int p) {
-        pin(node);
+        const cpu_set_t mine = pin(node);
+        struct Check {   // counts the thread as on its GPU's node if it ends its work there
+            const cpu_set_t &m;
+            std::atomic<uint32_t> &n;
+            ~Check() { if (on_node(m)) n.fetch_add(1); }
+        } check{mine, threads_on_node};
         for (uint64_t k = (uint64_t)p; k < nchunks_total && !abort.load(std::memory_order_relaxed); k += producers) {
             Chunk &cc = ch[k % c->chunks];
             for (unsigned spins = 0; cc.state.load(std::memory_order_acquire) != 3 * k; relax(spins))
@@ -342,7 +367,12 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     // consumers: transmit redirected frames (digest + byte count per egress), drop the rest
     std::vector<hfv_loop_stats> part(consumers);
     auto consume = [&](int q) {
-        pin(node);
+        const cpu_set_t mine = pin(node);
+        struct Check {
+            const cpu_set_t &m;
+            std::atomic<uint32_t> &n;
+            ~Check() { if (on_node(m)) n.fetch_add(1); }
+        } check{mine, threads_on_node};
         hfv_loop_stats &s = part[q];
         memset(&s, 0, sizeof s);
         for (uint64_t k = (uint64_t)q; k < nchunks_total && !abort.load(std::memory_order_relaxed); k += consumers) {
@@ -495,6 +525,9 @@ extern "C" int hfv_loop_run(hfv_ctx *ctx, const struct hfv_loop_config *c, struc
     if (rc) abort.store(true);
     for (auto &t : th) t.join();
     out->rx_truncated = rx_trunc.load();
+    out->numa_node = node;
+    out->threads = (uint32_t)(producers + consumers);
+    out->threads_on_node = threads_on_node.load();
     out->tx_errors = tx_err.load();
     close_sockets();
     const double t1 = now_s();

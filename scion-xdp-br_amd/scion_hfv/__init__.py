@@ -21,6 +21,9 @@ except Exception:  # pragma: no cover - torch is optional for C-style use
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libscionhfv.so")
+# the test build: the same library plus the test hooks (hfv_debug_relay_delay, _publish_delay,
+# _br_grid, _br_split, _loop_host_stage); loaded only by tests (HFV_LIB), never by the product path
+TEST_LIB_PATH = os.path.join(PKG_ROOT, "lib", "libscionhfv_test.so")
 
 KEYSEL_ZERO = 0
 KEYSEL_IFID = 1
@@ -243,7 +246,9 @@ class LoopStats(ctypes.Structure):
                 ("verdict_pkts", ctypes.c_uint64 * 11), ("seconds", ctypes.c_double),
                 ("gpu_busy_s", ctypes.c_double), ("gpu_wait_s", ctypes.c_double),
                 ("producer_busy_s", ctypes.c_double), ("consumer_busy_s", ctypes.c_double),
-                ("rx_truncated", ctypes.c_uint64), ("tx_errors", ctypes.c_uint64)]
+                ("rx_truncated", ctypes.c_uint64), ("tx_errors", ctypes.c_uint64),
+                ("numa_node", ctypes.c_int32), ("threads", ctypes.c_uint32), ("threads_on_node", ctypes.c_uint32),
+                ("pad_", ctypes.c_uint32)]
 
 
 def loop_run(handle, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, chunks=8, producers=2,
@@ -266,7 +271,8 @@ def loop_run(handle, frames, lens, total, rx_ifindex=1, slot=192, chunk=65536, c
     return {"rx": st.rx_pkts, "tx": st.tx_pkts, "tx_bytes": st.tx_bytes, "drop": st.drop_pkts,
             "tx_digest": st.tx_digest, "verdicts": list(st.verdict_pkts), "seconds": st.seconds,
             "gpu_busy_s": st.gpu_busy_s, "gpu_wait_s": st.gpu_wait_s, "producer_busy_s": st.producer_busy_s,
-            "consumer_busy_s": st.consumer_busy_s, "rx_truncated": st.rx_truncated, "tx_errors": st.tx_errors}
+            "consumer_busy_s": st.consumer_busy_s, "rx_truncated": st.rx_truncated, "tx_errors": st.tx_errors,
+            "numa_node": st.numa_node, "threads": st.threads, "threads_on_node": st.threads_on_node}
 
 
 # Test-only host router stage for hfv_loop_run (see hfv_loop.cpp): fn(frames, slot, len,
@@ -431,6 +437,18 @@ class Ctx:
         fin = [int(v[4 + 1024 + k]) for k in range(grid)]
         t0 = min(st)
         return [((a - t0) / 100.0, (b - t0) / 100.0) for a, b in zip(st, fin)]
+
+    def stream_read_ms(self, bufs, stream=None):
+        """Diagnostic (hfv_debug_stream_read): one dense non-temporal read of the device tensors
+        `bufs` (<= 64); returns its kernel time in ms."""
+        L = lib()
+        L.hfv_debug_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+        ptrs = (ctypes.c_void_p * len(bufs))(*[_ptr(b) for b in bufs])
+        sizes = (ctypes.c_size_t * len(bufs))(*[b.numel() * b.element_size() for b in bufs])
+        ms = ctypes.c_float(0.0)
+        _check(L.hfv_debug_stream_read(self._h, ptrs, sizes, len(bufs), _stream(stream), ctypes.byref(ms)))
+        return ms.value
 
     def verify_batches_timed(self, batches, stream=None):
         """verify_batches, waited for; returns the launches' execution time in ms."""

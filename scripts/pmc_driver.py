@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Workload for rocprofv3 --pmc passes: verify 2^20 and 2^24 records (config 2, and config 3
 with --keysel ifid), `reps` launches each, after one untimed generation pass.  With a 4th
-argument `svc` the batches go through the resident service instead: per size one 2-batch
+argument `bat` every size's `reps` batches go through one hfv_verify_batches call (twice; the
+first is dropped as the warm-up).  With a 4th argument `svc` the batches go through the resident service instead: per size one 2-batch
 grid (dropped by pmc_summary.py as the warm-up) and one grid of `reps` batches (`svcrun`: the
 same grids through hfv_service_run, every batch in the kernel arguments).  With a 5th
 argument `rotR` each size is held in R resident batches and batch k of a grid verifies
@@ -48,6 +49,7 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
     svc = len(sys.argv) > 4 and sys.argv[4] in ("svc", "svcrun")
+    bat = len(sys.argv) > 4 and sys.argv[4] == "bat"   # hfv_verify_batches: `reps` batches in one call
     run = len(sys.argv) > 4 and sys.argv[4] == "svcrun"   # the batches inline (hfv_service_run)
     rot = int(sys.argv[5][3:]) if len(sys.argv) > 5 and sys.argv[5].startswith("rot") else 1
     torch.cuda.set_device(0)
@@ -63,7 +65,12 @@ def main():
         bits = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(max(R, reps, 2))]
         for i, r in enumerate(recs):   # consecutive generator dispatches = one size group (pmc_summary.py)
             ctx.gen_records(r, n, SEED_RECORDS, first_index=i * n)
-        if svc:
+        if bat:   # two calls of `reps` batches: the first is dropped by pmc_summary.py as the warm-up
+            for _ in range(2):
+                ctx.verify_batches([(recs[j % R], n, bits[j]) for j in range(reps)])
+                torch.cuda.synchronize()
+                print(f"batches n={n} reps={reps} shader_mhz={ctx.batches_shader_mhz()}", flush=True)
+        elif svc:
             torch.cuda.synchronize()
             for k in (2, reps):
                 if run:

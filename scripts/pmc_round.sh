@@ -5,9 +5,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 KS=${1:-zero}
-SVC=${2:-}          # "svc": batches through the resident service (10 per grid)
+SVC=${2:-}          # "svc": batches through the resident service (10 per grid); "bat": 10 per hfv_verify_batches call
 ROT=${3:-rot1}      # "rot8": 8 resident 2^20 batches rotated, as in bench.py's headline
-OUT=gpurun_out/pmc_$KS${SVC:+_svc}_$ROT
+OUT=gpurun_out/pmc_$KS${SVC:+_$SVC}_$ROT
 mkdir -p $OUT
 groups=(
   "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
@@ -25,7 +25,9 @@ for g in "${groups[@]}"; do
   timeout -k 10 300 rocprofv3 --pmc $g --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
       python3 scripts/pmc_driver.py $KS 10 1048576,16777216 ${SVC:-launch} $ROT > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
-if [[ $SVC == svc ]]; then
+if [[ $SVC == bat ]]; then
+    python3 scripts/pmc_summary.py $OUT 1048576,16777216 k_verify_batches 10
+elif [[ $SVC == svc ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576,16777216 k_verify_service 10
 elif [[ $KS == br ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576 k_br_process

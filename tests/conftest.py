@@ -20,6 +20,22 @@ def pytest_configure(config):
         subprocess.run(["make", "-C", PKG], check=True, capture_output=True)
 
 
+def rerun_on_test_build(request, timeout=600):
+    """A test that needs a test hook (hfv_debug_relay_delay, _publish_delay, _br_grid, _br_split:
+    compiled into lib/libscionhfv_test.so only, never into the product library) runs in a child
+    pytest process on the test build.  Returns True in the parent (the child ran it and passed),
+    False in the child (run the test body)."""
+    if os.environ.get("HFV_TEST_BUILD_CHILD") == "1":
+        return False
+    import scion_hfv as hfv
+    env = dict(os.environ, HFV_LIB=hfv.TEST_LIB_PATH, HFV_TEST_BUILD_CHILD="1")
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu or not gpu",
+                        request.node.nodeid], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.stdout[-4000:], r.stderr[-2000:])
+    assert " passed" in r.stdout, r.stdout[-2000:]
+    return True
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     import torch

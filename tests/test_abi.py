@@ -37,7 +37,27 @@ def test_lib_exports_every_declared_symbol():
     assert not missing, missing
     assert "AES_SBox" in exported
     L = hfv.lib()
-    assert L.hfv_abi_version() == 2
+    assert L.hfv_abi_version() == 3
+
+
+TEST_HOOKS = ("hfv_debug_loop_host_stage", "hfv_debug_publish_delay", "hfv_debug_relay_delay", "hfv_debug_br_grid",
+              "hfv_debug_br_split")
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_test_hooks_only_in_the_test_build():
+    """the hooks that change what the library does (a host callback in place
+    of the router kernel, delays, launch-shape overrides) are compiled into the test build only;
+    the product library exports none of them, and its diagnostics are read-only."""
+    prod, test = _exports(hfv.LIB_PATH), _exports(hfv.TEST_LIB_PATH)
+    assert not prod & set(TEST_HOOKS), sorted(prod & set(TEST_HOOKS))
+    assert set(TEST_HOOKS) <= test
+    assert declared_functions() <= test            # the test build is the product plus the hooks
+    assert {s for s in prod if s.startswith("hfv_")} <= test
 
 
 def test_exported_sbox():
@@ -127,7 +147,7 @@ def test_new_entry_points_reject_bad_arguments_without_gpu():
     assert L.hfv_service_run(None, None, 0, ctypes.byref(t), ctypes.byref(ms)) == -errno.EINVAL
     assert L.hfv_verdict_counters(None, None, 64, 1, None, None, None) == -errno.EINVAL
     assert "NULL" in L.hfv_last_error().decode() or "null" in L.hfv_last_error().decode()
-    assert ctypes.sizeof(hfv.LoopStats) == 8 * (5 + hfv.BR_COUNTERS) + 8 * 5 + 8 * 2
+    assert ctypes.sizeof(hfv.LoopStats) == 8 * (5 + hfv.BR_COUNTERS) + 8 * 5 + 8 * 2 + 16
 
 
 def test_ctypes_layouts_match_the_c_header(tmp_path):
@@ -136,7 +156,8 @@ def test_ctypes_layouts_match_the_c_header(tmp_path):
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     checks = {"hfv_loop_config": (hfv.LoopConfig, ["rx_ifindex", "total", "dma", "stats", "rx_ifname", "idle_ms"]),
-              "hfv_loop_stats": (hfv.LoopStats, ["verdict_pkts", "seconds", "rx_truncated", "tx_errors"]),
+              "hfv_loop_stats": (hfv.LoopStats, ["verdict_pkts", "seconds", "rx_truncated", "tx_errors", "numa_node",
+                                                 "threads", "threads_on_node"]),
               "hfv_br_config": (hfv.BrConfig, ["egress", "routes", "tx_ports"])}
     src = ["#include <stdio.h>", "#include <stddef.h>", '#include "scion_hfv.h"', "int main(void) {"]
     for st, (_, fields) in checks.items():

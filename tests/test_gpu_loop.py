@@ -7,6 +7,7 @@ import pytest
 
 import orc
 import scion_hfv as hfv
+from conftest import rerun_on_test_build
 from scion_hfv import evaluation as E
 
 pytestmark = pytest.mark.gpu
@@ -61,12 +62,14 @@ def test_loop_matches_oracle(gpu_ctx, hf_check, dma):
 
 
 @pytest.mark.parametrize("dma", [0, 2], ids=["zero_copy", "dma_in_zc_out"])
-def test_loop_publish_races_second_stream(gpu_ctx, dma):
+def test_loop_publish_races_second_stream(request, gpu_ctx, dma):
     """The round-2 failure made deterministic: the table publish the loop's first chunk does on
     its stream is held 3 ms behind a spin kernel (hfv_debug_publish_delay), so chunk 1 on the
     loop's second stream launches while the copy of the new key and tables is still queued.
     It must wait for that copy (the publish fence); without it every MAC of chunk 1 fails
     against the stale key and tx falls short by one chunk (gpurun_out/r02c5)."""
+    if rerun_on_test_build(request):   # uses a test hook: runs on lib/libscionhfv_test.so
+        return
     import torch
     recs = torch.zeros((64, 64), dtype=torch.uint8, device="cuda:0")
     bits = torch.zeros(1, dtype=torch.int64, device="cuda:0")
@@ -88,11 +91,13 @@ def test_loop_publish_races_second_stream(gpu_ctx, dma):
 
 
 @pytest.mark.parametrize("dma", [0, 2], ids=["zero_copy", "dma_in_zc_out"])
-def test_loop_single_block_chunks(gpu_ctx, dma):
+def test_loop_single_block_chunks(request, gpu_ctx, dma):
     """The round-2 failing shape, forced: each 1000-frame chunk runs as ONE 1024-thread block
     whose 16 waves are all active (hfv_debug_br_grid(1)), zero-copy on the mapped ring, fresh
     router tables and key published by the loop's first chunk (the loop's other streams must
     wait for that publish).  Repeated so chunk 1 races the publish more than once."""
+    if rerun_on_test_build(request):   # uses a test hook: runs on lib/libscionhfv_test.so
+        return
     frames = _frame_mix(97, bad_every=5)
     stats = np.zeros((hfv.BR_STATS_IFINDEX, 2, hfv.BR_COUNTERS), dtype=np.uint64)
     want = _oracle(frames, 10007, True)

@@ -11,6 +11,7 @@ import pytest
 
 import orc
 import scion_hfv as hfv
+from conftest import rerun_on_test_build
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -402,13 +403,15 @@ def _grid_ms(ctx, posts):
 
 
 @pytest.mark.parametrize("k,n", [(20, 1 << 20), (100, 1 << 18)], ids=["k20_2e20", "k100_2e18"])
-def test_service_grid_ignores_host_round_trips(ctx, k, n):
+def test_service_grid_ignores_host_round_trips(request, ctx, k, n):
     """the resident grid must not run at the pace of host-memory round trips.
     A debug hook makes every host read of the relay wave take 30 us longer (a slow PCIe link,
     as on the driver's round-3 box, whose service grids ran at ~42 us per 2^20 batch).  K = 20
     batches all travel in the kernel arguments; K = 100 puts 36 behind the relay's read-ahead.
     Either way no block ever waits for a descriptor, the verdicts equal the launch path's, and
     the delayed grids stay within 1.5x of the undelayed ones (within noise in practice)."""
+    if rerun_on_test_build(request):   # uses a test hook: runs on lib/libscionhfv_test.so
+        return
     ctx.key_add(0, orc.KEY_1111)
     R = 4
     recs = [torch.empty((n, 64), dtype=torch.uint8, device=DEV) for _ in range(R)]
@@ -453,10 +456,12 @@ def test_service_grid_ignores_host_round_trips(ctx, k, n):
     assert slow <= 1.5 * fast, times
 
 
-def test_service_live_submits_with_slow_host_link(ctx):
+def test_service_live_submits_with_slow_host_link(request, ctx):
     """The relay's other duties under a slow host link (30 us extra per host read): descriptors
     posted one at a time to a running grid, and completions forwarded to the host ring so that
     hfv_service_wait and ring-slot reuse (more batches than ring slots) still work."""
+    if rerun_on_test_build(request):   # uses a test hook: runs on lib/libscionhfv_test.so
+        return
     g = orc.load_golden("hf_single.npz")
     n = len(g["records"])
     d = dev(g["records"])

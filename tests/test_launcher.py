@@ -54,7 +54,7 @@ def test_two_service_ranks_on_one_gpu():
     half the CUs (hfv_service_set_grid: CUs / ranks), both timed together; every bitmap is checked
     against the generator truth inside bench.py, and each rank reports its thread budget."""
     d = _bench("--gpus", "2", "--same-device", "--n", "262144", "--rotate", "2", "--steps", "8", "--warmup", "2",
-               "--no-extras", "--no-host-e2e", "--cpu-budget", "0.2", timeout=600)
+               "--no-extras", "--no-host-e2e", "--cpu-budget", "0.2", "--mode", "service", timeout=600)
     assert d["n_gpus"] == 1 and d["ranks"] == 2 and len(d["per_rank_ms"]["all"]) == 2
     # VERDICT r04 #6: the N > 1 line carries its CPU baseline (rank 0, after every rank's GPU legs)
     cb = d["cpu_baseline"]
@@ -71,6 +71,39 @@ def test_two_service_ranks_on_one_gpu():
     assert len(g) == 2 and all(0 < x < 1.0 for x in g), g
     assert max(g) < 2.5 * min(g), g
     assert all(r["block_waits"] == 0 for r in d["service"]["relay"]), d["service"]["relay"]
+
+
+@pytest.mark.gpu
+def test_two_loop_ranks_on_one_gpu():
+    """config 5 (hfv_loop_run: producer threads -> RX ring -> router kernel ->
+    TX/drop consumers) with two ranks at once, the way the driver's N > 1 run executes it (every
+    rank runs the loop leg; here both on GPU 0).  Per rank: rx/tx/drop/byte/verdict counts and the
+    order-free digest of every transmitted (rewritten) frame equal the oracle router's over the
+    same cyclic frame sequence, and every producer and consumer thread ended its work on a CPU of
+    the GPU's NUMA node.  The headline (batch-list) and service legs ran first on both ranks."""
+    import numpy as np
+    from scion_hfv import evaluation as E
+    from test_gpu_loop import _oracle
+    total = 300_000
+    d = _bench("--gpus", "2", "--same-device", "--n", "65536", "--rotate", "2", "--steps", "4", "--warmup", "2",
+               "--no-host-e2e", "--cpu-budget", "0", "--big-n", "0", "--br-n", "0", "--loop-n", str(total),
+               "--loop-chunk", "16384", "--loop-chunks", "6", "--loop-threads", "3", "--loop-consumers", "2",
+               "--loop-digest", timeout=900)
+    assert d["n_gpus"] == 1 and d["ranks"] == 2
+    loop = d["config5_loop"]
+    assert "error" not in loop, loop
+    want = _oracle(E.frames(1000), total)
+    per = loop["per_rank"]
+    assert [p["rank"] for p in per] == [0, 1]
+    for p in per:
+        assert p["error"] is None, p
+        for k in ("rx", "tx", "tx_bytes", "drop", "verdicts"):
+            assert p[k] == want[k], (p["rank"], k, p[k], want[k])
+        assert int(p["tx_digest"], 16) == want["tx_digest"], p["rank"]
+        assert p["threads"] >= 2
+        if p["numa_node"] >= 0:
+            assert p["threads_on_node"] == p["threads"], p
+    assert loop["mpkts"] > 0 and np.isfinite(loop["mpkts"])
 
 
 @pytest.mark.gpu

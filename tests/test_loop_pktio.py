@@ -17,8 +17,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _child(n):
+    import scion_hfv as hfv
+    # the host router stage is a test hook: the child loads the test build of the library
     r = subprocess.run([sys.executable, os.path.join(HERE, "pktio_loop_child.py"), str(n)], capture_output=True,
-                       text=True, timeout=240, env=dict(os.environ, OMP_NUM_THREADS="1"))
+                       text=True, timeout=240, env=dict(os.environ, OMP_NUM_THREADS="1", HFV_LIB=hfv.TEST_LIB_PATH))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert lines, r.stdout[-2000:] + r.stderr[-2000:]

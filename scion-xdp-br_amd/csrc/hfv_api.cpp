@@ -254,7 +254,6 @@ struct hfv_ctx {
     SvcWeights svc_w_used = svc_w;   // the running / last grid's
     bool svc_adapt = false;          // the running grid got all its batches up front (svc_run): measure it
     std::vector<uint64_t> svc_run_ns;   // ... their record counts
-    struct timespec svc_launch_ts = {0, 0};   // host clock at the running grid's launch call
     uint64_t svc_call_ns[6] = {0, 0, 0, 0, 0, 0};   // hfv_debug_service_call_ns: the last svc_run's phases
 };
 
@@ -1770,13 +1769,20 @@ static int svc_post(hfv_ctx *ctx, uint64_t recs, uint64_t bits, uint64_t n, uint
 // time from table fill to its last completed share is its verify rate).  Weights follow the
 // XCDs' mean rates (block j on XCD j % 8) and block 0's own, averaged with the previous weights
 // (halves run-to-run noise), clamped to [1/2, 2] of nominal.  Grids shorter than 50 us carry
-// too little signal and leave them alone: with the grid's wall time from the host's clock
-// (ns) below that, the stamps are not even copied (a synchronous 16 KiB copy after
-// every short grid).
+// too little signal and leave them alone: with the grid's duration (grid_ns: its dispatch events;
+// < 0 when it was not timed, then block 0's own stamps) below that, the G stamps are not even
+// copied (a synchronous 16 KiB copy after every short grid).
 static void svc_balance(hfv_ctx *ctx, double grid_ns)
 {
     const uint64_t G = ctx->svc_grid;
-    if (G < 16 || ctx->svc_run_ns.empty() || grid_ns < 50000.0) return;
+    if (G < 16 || ctx->svc_run_ns.empty()) return;
+    if (grid_ns >= 0.0 && grid_ns < 50000.0) return;
+    if (grid_ns < 0.0) {   // untimed grid: block 0's span first (s_memrealtime, 100 MHz)
+        uint64_t b0[2] = {0, 0};
+        if (svc_dev_read(ctx, &b0[0], offsetof(SvcDev, blk_start), 8) ||
+            svc_dev_read(ctx, &b0[1], offsetof(SvcDev, blk_fin), 8) || b0[1] < b0[0] + 5000)
+            return;
+    }
     std::vector<uint64_t> bt(2 * kSvcMaxBlocks);   // blk_start[0..G), blk_fin[0..G) (adjacent in SvcDev)
     static_assert(offsetof(SvcDev, blk_fin) == offsetof(SvcDev, blk_start) + kSvcMaxBlocks * 8, "layout");
     if (svc_dev_read(ctx, bt.data(), offsetof(SvcDev, blk_start), G * 8) ||
@@ -1866,9 +1872,13 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     if (rc) return rc;
     if (kernel_ms && ctx->svc_timed) HIP_TRY(hipEventElapsedTime(kernel_ms, ctx->svc_ev[0], ctx->svc_ev[1]));
     if (ctx->svc_adapt && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) {
-        struct timespec t1;
-        clock_gettime(CLOCK_MONOTONIC, &t1);
-        svc_balance(ctx, (t1.tv_sec - ctx->svc_launch_ts.tv_sec) * 1e9 + (t1.tv_nsec - ctx->svc_launch_ts.tv_nsec));
+        // the grid's own duration decides whether its stamps carry signal (the host
+        // time since the launch call can be far longer than the grid ran): its dispatch events when
+        // it was timed, else block 0's stamps (two words) before all G stamps are fetched
+        double grid_ns = -1.0;
+        float ms = 0.0f;
+        if (ctx->svc_timed && hipEventElapsedTime(&ms, ctx->svc_ev[0], ctx->svc_ev[1]) == hipSuccess) grid_ns = ms * 1e6;
+        svc_balance(ctx, grid_ns);
     }
     ctx->svc_adapt = false;
     // A grid that left on the stop descriptor verified every batch before it (each block
@@ -1879,7 +1889,15 @@ static int svc_stop(hfv_ctx *ctx, float *kernel_ms)
     if (__atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) == 0) return 0;
     std::vector<uint64_t> done;
     rc = svc_read_done(ctx, done);
-    if (rc) return rc;
+    if (rc) {
+        // the completion words cannot be read: every ticket that may still have been open is
+        // recorded as lost, so no poll or wait reports it done (fail closed)
+        for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t) {
+            if (ctx->svc_lost.size() >= 4096) ctx->svc_lost.erase(ctx->svc_lost.begin(), ctx->svc_lost.begin() + 1024);
+            ctx->svc_lost.push_back(ctx->svc_base + t - 1);
+        }
+        return rc;
+    }
     uint64_t first_lost = 0;
     for (uint64_t t = last; t > 0 && t + kSvcRing > last; --t)
         if (!svc_dev_done(ctx, done, t)) {
@@ -1960,7 +1978,9 @@ static inline uint64_t mono_ns()
     return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
 }
 
-static int svc_launch(hfv_ctx *ctx, DevState *ds)
+// call_ns (nullable): svc_run's phase stamps (hfv_debug_service_call_ns), [3] before and [4] after
+// the launch call; other callers (submitv, start) leave them alone
+static int svc_launch(hfv_ctx *ctx, DevState *ds, uint64_t *call_ns = nullptr)
 {
     const bool noev = !ctx->svc_timing;
     ctx->svc_timed = !noev;
@@ -1991,15 +2011,14 @@ static int svc_launch(hfv_ctx *ctx, DevState *ds)
     for (int r = 0; r < kDevKeyRows; ++r) memcpy(&a.key0[4 * r], ctx->host_img->keys.rows[r][0], 16);
     a.key0_ok = ctx->host_img->keys.valid[0] & 1u;
     memcpy(a.t0, kTables.t0, sizeof a.t0);
-    ctx->svc_call_ns[3] = mono_ns();
+    if (call_ns) call_ns[3] = mono_ns();
     int e = launch_verify_service(ctx->geom, ctx->keysel, a, ctx->svc_stream, noev ? nullptr : ctx->svc_ev[0],
                                   noev ? nullptr : ctx->svc_ev[1], &ctx->svc_grid);
-    ctx->svc_call_ns[4] = mono_ns();
+    if (call_ns) call_ns[4] = mono_ns();
     int rc = after_launch(ctx, ctx->svc_stream, e, "verify service launch");
     if (rc) return rc;
     ++ctx->svc_launches;
     ctx->svc_running = true;
-    clock_gettime(CLOCK_MONOTONIC, &ctx->svc_launch_ts);   // bounds the grid's life from above (svc_balance)
     return 0;
 }
 
@@ -2148,6 +2167,9 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
     bool launched = false;
     for (size_t i = 0; i <= count && !rc; ++i) {
         if (!launched && ctx->svc_next > (uint64_t)kSvcRing) {
+            // a run longer than the ring: the grid is launched mid-post, so the phase stamps of
+            // this call would mix posting and launching -- they are left at 0 for it
+            memset(ctx->svc_call_ns, 0, sizeof ctx->svc_call_ns);
             rc = svc_launch(ctx, ds);
             launched = true;
             if (rc) break;
@@ -2163,10 +2185,10 @@ static int svc_run(hfv_ctx *ctx, const struct hfv_batch *batches, size_t count, 
         if (i == 0) *first_ticket = t;
     }
     if (!launched) {
-        int lr = svc_launch(ctx, ds);
+        int lr = svc_launch(ctx, ds, ctx->svc_call_ns);
         if (lr) return lr;
+        ctx->svc_call_ns[5] = mono_ns();
     }
-    ctx->svc_call_ns[5] = mono_ns();
     if (!wait) return rc;   // the grid exits after the stop posted behind the batches
     int sr = svc_stop(ctx, kernel_ms);
     return rc ? rc : sr;
@@ -2176,13 +2198,19 @@ int hfv_service_poll(hfv_ctx *ctx, uint64_t ticket)
 {
     if (!ctx) return fail(-EINVAL, "ctx is NULL");
     int st = svc_ticket_state(ctx, ticket);
-    if (st == 0 && ctx->svc_running && hipStreamQuery(ctx->svc_stream) == hipSuccess) {
-        // The grid is gone without its stop (idle timeout or watchdog): its relay wave stopped
-        // forwarding completions when it published the stop, so the host ring may never show
-        // this ticket.  Reap the grid: svc_stop reads the device completion words and records
-        // the tickets it left unverified (a poll loop never ended).
+    // A pending ticket of a grid that left without its stop (idle timeout or watchdog: the grid
+    // sets the status word in pinned memory first) would never complete: its relay wave stopped
+    // forwarding completions when it published the stop.  Only then (a read of pinned memory
+    // decides it, no HIP call on the poll path) reap the grid: svc_stop reads the
+    // device completion words and records the tickets it left unverified.
+    if (st == 0 && ctx->svc_running && __atomic_load_n(&ctx->svc_host->status, __ATOMIC_ACQUIRE) != 0 &&
+        hipStreamQuery(ctx->svc_stream) == hipSuccess) {
         DeviceGuard g(ctx->device);
-        (void)svc_stop(ctx, nullptr);
+        const int rc = svc_stop(ctx, nullptr);
+        // -ETIMEDOUT: the grid left tickets unverified, now recorded as lost (poll reports -EIO for
+        // those below).  Any other failure means the lost tickets could not be read: report it rather
+        // than fall through to a state that would call them done (fail closed).
+        if (rc && rc != -ETIMEDOUT) return rc;
         st = svc_ticket_state(ctx, ticket);
     }
     if (st == -EINVAL) return fail(-EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
@@ -2312,7 +2340,8 @@ int hfv_debug_feed_loop(hfv_ctx *ctx, const struct hfv_batch *b, size_t count, u
 // Diagnostic (not part of include/scion_hfv.h): the host-side phases of the last
 // hfv_service_run / run_async call in nanoseconds: [0] argument checks and stopping a previous
 // grid, [1] the new grid's bookkeeping (svc_begin), [2] posting the batches and building the
-// kernel arguments, [3] the launch call itself, [4] the rest (ticket state) to the return.
+// kernel arguments, [3] the launch call itself, [4] the rest (ticket state) to the return.  All 0
+// for a call with more batches than the ring holds (its grid is launched mid-post).
 int hfv_debug_service_call_ns(hfv_ctx *ctx, uint64_t out[5])
 {
     if (!ctx || !out) return fail(-EINVAL, "bad argument");

@@ -425,6 +425,7 @@ def test_service_grid_ignores_host_round_trips(request, ctx, k, n):
     torch.cuda.synchronize()
     posts = ctx.service_batches([(recs[i % R], n, outs[i]) for i in range(k)])
     times = {0: [], 30: []}
+    cycles = {0: [], 30: []}   # grid time x block 0's shader clock: the clock-independent check
     try:
         _grid_ms(ctx, posts)   # warm-up grid
         for _ in range(3):
@@ -434,6 +435,9 @@ def test_service_grid_ignores_host_round_trips(request, ctx, k, n):
                     o.fill_(-1)
                 torch.cuda.synchronize()
                 times[us].append(_grid_ms(ctx, posts))
+                mhz = ctx.service_shader_mhz()
+                if mhz:
+                    cycles[us].append(times[us][-1] * 1e3 * mhz)
                 rel = ctx.service_relay()
                 assert rel["block_waits"] == 0, rel
                 assert rel["inline"] == min(k + 1, hfv.SVC_INLINE), rel
@@ -454,6 +458,11 @@ def test_service_grid_ignores_host_round_trips(request, ctx, k, n):
     # the timing bound is loose (clocks vary on a shared box) but still catches a grid
     # at the pace of the delayed round trips (round 3's fault: 3-4x)
     assert slow <= 1.5 * fast, times
+    # the same comparison in shader cycles (the box's clock varies from grid to grid,
+    # the work per cycle does not), so a regression well below 1.5x is caught too
+    if len(cycles[0]) == 3 and len(cycles[30]) == 3:
+        cf, cs = sorted(cycles[0])[1], sorted(cycles[30])[1]
+        assert cs <= 1.2 * cf, cycles
 
 
 def test_service_live_submits_with_slow_host_link(request, ctx):

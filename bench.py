@@ -562,6 +562,32 @@ def service_legs(hfv, W, ctx, m, n, first, rotate, steps):
                         "note": f"{SUSTAINED_GRIDS} back-to-back service grids of {K} resident batches (k % {R}) each; "
                                 f"median of the last {len(tail)}: the clock the power limit holds under continuous "
                                 f"verify; frac per GPU"}
+    # the same continuous load through the headline path: back-to-back hfv_verify_batches calls of
+    # K batches each (one launch per 64 batches), each call timed by its launches' events
+    bgrids = []
+    for b in bms:
+        b.zero_()
+    for _ in range(SUSTAINED_GRIDS):
+        b_ms = ctx.verify_batches_timed(posts)
+        bgrids.append((b_ms, ctx.batches_shader_mhz() or 0.0))
+    W.sync()
+    for k in range(K):
+        assert torch.equal(bms[k], truth[k % R]), f"sustained (batches): bitmap {k} != generator truth"
+    btail = sorted(bgrids[len(bgrids) // 2:])
+    bg_ms, bmhz = btail[len(btail) // 2]
+    bg_all = W.gather(bg_ms)
+    bach = BYTES_PER_PACKET * n * K / (max(bg_all) * 1e-3) / 1e9
+    out["sustained_batches"] = {"batches_per_call": K, "calls": SUSTAINED_GRIDS, "kernel_ms": round(bg_ms, 4),
+                                "launches_per_call": -(-K // 64),
+                                "mpkts": round(W.size * n * K / max(bg_all) / 1e3, 1),
+                                "frac": round(bach / HBM_PEAK_GBS / W.size, 4),
+                                "shader_mhz": round(bmhz, 1) if bmhz else None,
+                                "all_calls_ms": [round(x[0], 4) for x in bgrids],
+                                "all_calls_mhz": [round(x[1], 1) for x in bgrids],
+                                "per_rank_kernel_ms": [round(x, 4) for x in bg_all],
+                                "note": f"{SUSTAINED_GRIDS} back-to-back hfv_verify_batches calls of {K} resident batches "
+                                        f"each, one host wait between calls; median of the "
+                                        f"last {len(btail)}; frac per GPU"}
     del bms
     # per_call: the documented feeder loop on a running grid
     bms = [torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda") for _ in range(steps)]

@@ -820,8 +820,8 @@ int hfv_verify_batches_timed(hfv_ctx *ctx, const struct hfv_batch *batches, size
 
 // Diagnostic (not part of include/scion_hfv.h): block 0's shader clock (s_memtime) and 100 MHz
 // s_memrealtime at the start and at the end of the last hfv_verify_batches launch (out[0..3]);
-// with words >= 4 + 2 * 1024 also every block's s_memrealtime after its table fill (out[4 + k]) and
-// when it finished (out[4 + 1024 + k]).  The caller has synchronized that launch.
+// with words >= 4 + 2 * 1024 also every block's s_memrealtime at its entry (out[4 + k]) and when it
+// finished (out[4 + 1024 + k]).  The caller has synchronized that launch.
 extern "C" int hfv_debug_batches_clock(hfv_ctx *ctx, uint64_t *out, size_t words)
 {
     if (!ctx || !out || words < 4) return fail(-EINVAL, "bad argument");

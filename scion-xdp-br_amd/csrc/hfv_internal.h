@@ -273,8 +273,8 @@ struct BatchArgs {
     uint32_t inf_off, hf_off;
     uint32_t nb, total;       // batches; tiles over all of them (< 2^32: 288 GB of records at stride 8 is 2^29 tiles)
     // nullable (diagnostics): [0..3] block 0's s_memtime / s_memrealtime at its start and at its end
-    // (wave 0); [4 + k] block k's s_memrealtime after its table fill, [4 + kBatchStampBlocks + k]
-    // when its last wave left (atomic max: the host zeroes it before the launch)
+    // (wave 0); [4 + k] block k's s_memrealtime at its entry, [4 + kBatchStampBlocks + k] when its
+    // last wave left (atomic max: the host zeroes it before a timed launch)
     uint64_t *clk;
     uint32_t key0[kDevKeyRows * 4];
     uint32_t key0_ok, pad_[3];

@@ -311,9 +311,14 @@ __global__ __launch_bounds__(kBlock) void k_verify_batches(const BatchArgs args)
     const uint32_t last = b1 - 1;
     const uint32_t inf_off = a->inf_off, hf_off = a->hf_off;
     UniformKey ukey(a->key0, a->key0_ok);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a->clk) {   // diagnostics: the shader clock over the grid
-        a->clk[0] = __builtin_amdgcn_s_memtime();
-        a->clk[1] = __builtin_amdgcn_s_memrealtime();
+    // diagnostics, stored before the first record loads are issued (a store issued after them would
+    // make the loop's first reuse of its data registers wait for every load ahead of it: vmcnt(0))
+    if (threadIdx.x == 0 && a->clk) {
+        a->clk[4 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();   // the block's entry
+        if (blockIdx.x == 0) {                                         // the shader clock over the grid
+            a->clk[0] = __builtin_amdgcn_s_memtime();
+            a->clk[1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
     if (threadIdx.x == 0) s_next_tile = kWaves;
     auto at = [&](uint32_t x) { return x < b1 ? x : last; };   // the tile a load reads for claim x
@@ -322,59 +327,71 @@ __global__ __launch_bounds__(kBlock) void k_verify_batches(const BatchArgs args)
         if (lane == 0) c = atomicAdd(&s_next_tile, 1u);
         return b0 + wave_uniform(c);
     };
-    uint32_t g = b0 + wv;   // the wave's first tile (static), its loads in flight while the tables are written
-    BatchTile cb;
-    cb.hi = 0;
-    cb.j = ~0u;             // batch_map starts its search at batch 0
-    batch_map(a, at(g), cb);
-    RecWords cur = batch_load(cb, at(g), lane, inf_off, hf_off);
-    uint32_t g1 = 0;
-    BatchTile nb1 = cb;
-    RecWords r1 = cur;
-    if constexpr (DEPTH == 2) {
-        g1 = claim();
-        batch_map(a, at(g1), nb1);
-        r1 = batch_load(nb1, at(g1), lane, inf_off, hf_off);
+    // Record buffers: the loop is unrolled DEPTH + 1 times over DEPTH + 1 fixed register slots, slot
+    // u verified in step u while the loads of the tile DEPTH claims ahead land in the slot step u - 1
+    // just verified -- so no loop-carried register copy (which would wait for the loads it copies,
+    // a vmcnt(0) at the latch) stands between a tile's loads and its use.
+    constexpr int S = DEPTH + 1;
+    RecWords buf[S];
+    BatchTile bt[S];
+    uint32_t gg[S];
+    gg[0] = b0 + wv;        // the wave's first tile (static), its loads in flight while the tables are written
+    bt[0].hi = 0;
+    bt[0].j = ~0u;          // batch_map starts its search at batch 0
+    batch_map(a, at(gg[0]), bt[0]);
+    buf[0] = batch_load(bt[0], at(gg[0]), lane, inf_off, hf_off);
+#pragma unroll
+    for (int d = 1; d < DEPTH; ++d) {
+        gg[d] = claim();
+        bt[d] = bt[d - 1];
+        batch_map(a, at(gg[d]), bt[d]);
+        buf[d] = batch_load(bt[d], at(gg[d]), lane, inf_off, hf_off);
     }
     fill_block<KEYSEL>(a->t0, a->tab, kBlock);
     __syncthreads();
-    if (threadIdx.x == 0 && a->clk) a->clk[4 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const Lane l = lane_bases();
-    const bool keyok = KEYSEL != HFV_KEYSEL_ZERO || ukey.ok;   // slot 0 empty: fail closed (xdp.c:83-84)
     // verdict words wait in a per-wave stash (lane k: the wave's k-th tile, with its own bitmap
     // address, since a wave's tiles may belong to two batches) and go out as one scattered store
     uint64_t st_word = 0, st_addr = 0;
     uint32_t stashed = 0;
-    while (g < b1) {
-        const uint32_t ng = claim();
-        BatchTile nb = DEPTH == 2 ? nb1 : cb;
-        batch_map(a, at(ng), nb);
-        const RecWords rn = batch_load(nb, at(ng), lane, inf_off, hf_off);
-        const uint64_t rec = (uint64_t)(g - cb.lo) * 64 + lane;
-        uint64_t ballot = 0;
-        if (keyok) ballot = verify_tile<KEYSEL, HFV_BATCH_PIN != 0>(cur, rec < cb.n, l, &ukey);
-        if (lane == stashed) {
-            st_word = ballot;
-            st_addr = cb.bits + (uint64_t)(g - cb.lo) * 8;
-        }
-        if (++stashed == 64) {
-            *(GlobalU64 *)st_addr = st_word;
-            stashed = 0;
-        }
-        if constexpr (DEPTH == 2) {
-            cur = r1;
-            cb = nb1;
-            g = g1;
-            r1 = rn;
-            nb1 = nb;
-            g1 = ng;
-        } else {
-            cur = rn;
-            cb = nb;
-            g = ng;
+    // KEYSEL_ZERO with slot 0 empty fails every packet closed (xdp.c:83-84): a loop of its own after
+    // the tile loop (a verify skipped inside the tile loop would leave the prefetched loads unconsumed
+    // on that path, and a store on a path into the loop's header would make its first register reuse
+    // wait for it: either way the waitcnt pass drains every load at the loop top)
+    const bool fail_closed = KEYSEL == HFV_KEYSEL_ZERO && !ukey.ok;
+    // the exits leave the unrolled body straight to `done` (a flag checked at the loop top would
+    // route them through the loop's header, whose waitcnt state would then hold the loads they left
+    // in flight: a vmcnt(0) there on every iteration)
+    if (gg[0] >= b1 || fail_closed) goto done;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+            const int in_slot = (u + DEPTH) % S, prev = (u + DEPTH - 1) % S;   // the free slot, the newest mapped
+            gg[in_slot] = claim();
+            bt[in_slot] = bt[prev];
+            batch_map(a, at(gg[in_slot]), bt[in_slot]);
+            buf[in_slot] = batch_load(bt[in_slot], at(gg[in_slot]), lane, inf_off, hf_off);
+            const uint64_t rec = (uint64_t)(gg[u] - bt[u].lo) * 64 + lane;
+            const uint64_t ballot = verify_tile<KEYSEL, HFV_BATCH_PIN != 0>(buf[u], rec < bt[u].n, l, &ukey);
+            if (lane == stashed) {
+                st_word = ballot;
+                st_addr = bt[u].bits + (uint64_t)(gg[u] - bt[u].lo) * 8;
+            }
+            if (++stashed == 64) {
+                *(GlobalU64 *)st_addr = st_word;
+                stashed = 0;
+            }
+            if (gg[(u + 1) % S] >= b1) goto done;   // claims only grow: every later slot is past the range too
         }
     }
+done:
     if (lane < stashed) *(GlobalU64 *)st_addr = st_word;
+    if (fail_closed) {   // the block's verdict words are 0
+        for (uint32_t g = b0 + wv; g < b1; g += kWaves) {
+            batch_map(a, g, bt[0]);
+            if (lane == 0) *(GlobalU64 *)(bt[0].bits + (uint64_t)(g - bt[0].lo) * 8) = 0;
+        }
+    }
     if (lane == 0 && a->clk)   // the block's last wave to leave sets its finish stamp
         __hip_atomic_fetch_max(&a->clk[4 + kBatchStampBlocks + blockIdx.x], __builtin_amdgcn_s_memrealtime(),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -426,8 +426,8 @@ class Ctx:
         return (t1 - t0) / ((r1 - r0) / 100.0) if r1 > r0 and t1 > t0 else None
 
     def batches_block_span(self, grid):
-        """Diagnostic: per block of the last timed verify_batches launch, (fill done, finished) in
-        us after the earliest fill; None if unavailable."""
+        """Diagnostic: per block of the last timed verify_batches launch, (entered, finished) in
+        us after the earliest entry; None if unavailable."""
         v = (ctypes.c_uint64 * (4 + 2 * 1024))()
         L = lib()
         L.hfv_debug_batches_clock.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]

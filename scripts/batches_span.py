@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Where a hfv_verify_batches launch's time goes (diagnostic, not used by tests or the bench):
 K batches of 2^20 rotated resident records in one call, timed with the dispatch events, and
-every block's s_memrealtime after its table fill and when its last wave left.  Prints per
-launch: kernel ms, block 0's shader clock, the fill-done spread, the finish spread and the
+every block's s_memrealtime at its entry and when its last wave left.  Prints per
+launch: kernel ms, block 0's shader clock, the entry spread, the finish spread and the
 per-XCD (block % 8) mean finish.
     python scripts/batches_span.py [K] [reps]"""
 import os
@@ -38,7 +38,7 @@ def main():
         st = [a for a, _ in span]
         fin = [b for _, b in span]
         xcd = [statistics.mean(fin[x::8]) for x in range(8)]
-        print(f"kernel {ms * 1e3:7.1f} us  mhz {mhz:6.0f}  fill-done spread {max(st) - min(st):5.1f} us  "
+        print(f"kernel {ms * 1e3:7.1f} us  mhz {mhz:6.0f}  entry spread {max(st) - min(st):5.1f} us  "
               f"finish min/med/max {min(fin):6.1f} {statistics.median(fin):6.1f} {max(fin):6.1f} us  "
               f"per-XCD mean finish {' '.join(f'{x:6.1f}' for x in xcd)}", flush=True)
     torch.cuda.synchronize()

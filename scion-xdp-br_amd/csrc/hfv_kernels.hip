@@ -1281,6 +1281,25 @@ int launch_verify_records(const LaunchGeom &g, const DevKeyTable *tab, const Dev
                           size_t stride, size_t n, uint32_t inf_off, uint32_t hf_off, uint64_t *bits, void *stream,
                           void *ev_start, void *ev_stop, bool interleaved)
 {
+    // Records in device memory: the batch-list kernel with one batch (the same loop as a burst of
+    // batches, hfv_verify_batches; its 32-bit lane offsets and tile numbers bound stride and n).
+    if (!interleaved && stride <= ((size_t)1 << 24) && n <= ((size_t)1 << 36)) {
+        BatchArgs a;
+        memset(&a, 0, sizeof a);
+        a.tab = tab;
+        a.inf_off = inf_off;
+        a.hf_off = hf_off;
+        a.nb = 1;
+        a.total = (uint32_t)((n + 63) / 64);
+        a.cum[0] = 0;
+        a.cum[1] = a.total;
+        a.d[0] = {(uint64_t)(uintptr_t)recs, (uint64_t)(uintptr_t)bits, (uint64_t)n, (uint64_t)stride};
+        const RecArgs ra = rec_args(host_keys);
+        memcpy(a.key0, ra.key0, sizeof a.key0);
+        a.key0_ok = ra.key0_ok;
+        memcpy(a.t0, ra.t0, sizeof a.t0);
+        return launch_verify_batches(g, keysel, a, stream, ev_start, ev_stop);
+    }
     using K = void (*)(const DevKeyTable *, const uint8_t *, uint64_t, uint64_t, uint32_t, uint32_t, uint64_t *,
                        uint64_t *, const RecArgs);
     const bool ifid = keysel == HFV_KEYSEL_IFID;

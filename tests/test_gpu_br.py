@@ -73,6 +73,21 @@ def test_ipv4_options_across_the_window(gpu_ctx):
     assert (v == v[0]).all() and (v[0] == hfv.VERDICT["SCION_FORWARD"]).sum() >= m // 2
 
 
+@pytest.mark.parametrize("hdrlen", [0, 23, 255])
+def test_hdrlen_hint_across_the_window(gpu_ctx, hdrlen):
+    """The kernel loads bytes 128-135 early for a frame whose SCION header, by its HdrLen, runs
+    past the staging window (a hint only: the router never checks HdrLen).  With every frame's
+    HdrLen forced to 0 (no early load: every read past the window goes to HBM), 23 (92 bytes:
+    the load for the frames shifted by IPv4 options) or 255 (the load for every frame) the
+    results stay bit-exact against the oracle, frames inside, across and past the window."""
+    brs = {b: T.OracleBR(T.br_config(b, False)) for b in ("br1", "br2", "br3")}
+    frames, lens, ifidx, m = F.options_shift_batch(F.hop_inputs(brs, False, MAC))
+    for i in range(len(frames)):
+        sc = 14 + 4 * (frames[i, 14] & 15) + 8
+        frames[i, sc + 5] = hdrlen
+    _compare(gpu_ctx, frames, lens, ifidx, T.br_config("br1"), T.KEYS[1])
+
+
 @pytest.mark.parametrize("v6", [False, True], ids=["ipv4", "ipv6"])
 @pytest.mark.parametrize("br", ["br1", "br2", "br3"])
 def test_fuzz_parity(gpu_ctx, br, v6):

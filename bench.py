@@ -1254,7 +1254,8 @@ def run_hf(args, W):
                              "batches_frac": round(bytes_per_batch * args.steps / (m3["bat_kernel_ms"] * 1e-3) / 1e9
                                                    / HBM_PEAK_GBS, 4),
                              "batches_mpkts": round(total * args.steps / m3["bat_el"] / 1e6, 2),
-                             "ceilings": ceilings("ifid", n, m3["mhz"], cus, "service")}
+                             "ceilings": ceilings("ifid", n, m3["mhz"], cus, "service"),
+                             "batches_ceilings": ceilings("ifid", n, m3["bat_mhz"], cus, "batches")}
         del m3
         ctx3.close()
 

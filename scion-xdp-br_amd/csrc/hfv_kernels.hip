@@ -1046,21 +1046,6 @@ __global__ __launch_bounds__(kBlock) void k_verify_service(const SvcArgs args)
     }
 }
 
-// Diagnostics (hfv_debug_publish_delay): hold a stream for `us` microseconds, bounded by the
-// 100 MHz s_memrealtime, so a test can queue a key-table publish behind it deterministically.
-__global__ void k_debug_spin(uint32_t us)
-{
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * us) __builtin_amdgcn_s_sleep(8);
-}
-
-int launch_debug_spin(void *stream, uint32_t us)
-{
-    if (us > 1000000u) us = 1000000u;
-    hipLaunchKernelGGL(k_debug_spin, dim3(1), dim3(64), 0, (hipStream_t)stream, us);
-    return (int)hipGetLastError();
-}
-
 int launch_verify_service(const LaunchGeom &g, int keysel, const SvcArgs &args, void *stream, void *ev_start,
                           void *ev_stop, unsigned *grid_out)
 {

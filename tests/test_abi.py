@@ -58,6 +58,8 @@ def test_test_hooks_only_in_the_test_build():
     assert set(TEST_HOOKS) <= test
     assert declared_functions() <= test            # the test build is the product plus the hooks
     assert {s for s in prod if s.startswith("hfv_")} <= test
+    # the spin kernel behind the publish delay lives in the test build's own object
+    assert not [s for s in prod if "debug_spin" in s] and [s for s in test if "debug_spin" in s]
 
 
 def test_exported_sbox():

@@ -49,6 +49,18 @@ def test_two_product_ranks_on_one_gpu():
 
 
 @pytest.mark.gpu
+def test_two_batch_list_ranks_on_one_gpu():
+    """The default headline (one hfv_verify_batches launch per K steps) with two ranks on GPU 0:
+    each rank's launches use the whole chip and share it with the other's; every bitmap is
+    checked against the generator truth inside bench.py; the line reports both ranks."""
+    d = _bench("--gpus", "2", "--same-device", "--n", "262144", "--rotate", "2", "--steps", "8", "--warmup", "2",
+               "--no-extras", "--no-host-e2e", "--cpu-budget", "0", timeout=600)
+    assert d["n_gpus"] == 1 and d["ranks"] == 2 and len(d["per_rank_ms"]["all"]) == 2
+    assert d["roofline"]["kernel"] == "k_verify_batches" and d["value"] > 0
+    assert d["batches"]["kernel_ms"] > 0
+
+
+@pytest.mark.gpu
 def test_two_service_ranks_on_one_gpu():
     """the service path with two ranks on GPU 0, each resident grid limited to
     half the CUs (hfv_service_set_grid: CUs / ranks), both timed together; every bitmap is checked

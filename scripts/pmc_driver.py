@@ -18,8 +18,9 @@ import scion_hfv as hfv  # noqa: E402
 from bench import KEY_1111, SEED_RECORDS, key_table_256  # noqa: E402
 
 
-def run_br(reps, n=1 << 20):
-    """Config 4: the bench frame mix through hfv_br_process, reps launches on fresh copies."""
+def run_br(reps, n=1 << 20, one=False):
+    """Config 4: the bench frame mix through hfv_br_process, reps launches on fresh copies
+    (one=True, `br1t`: every frame the bench mix's first template -- no divergence)."""
     from bench import BR_SLOT, br_batch
     from scion_hfv import topology as TP
     torch.cuda.set_device(0)
@@ -27,6 +28,8 @@ def run_br(reps, n=1 << 20):
     ctx.key_add(0, TP.KEYS[1])
     ctx.br_set_config(TP.br_config("br1"))
     tmpl, tid, lens, ifidx, _ = br_batch(n, 0)
+    if one:
+        tid[:], lens[:], ifidx[:] = tid[0], lens[0], ifidx[0]
     master = torch.from_numpy(tmpl).cuda()[torch.from_numpy(tid.astype("int64")).cuda()]
     d_len = torch.from_numpy(lens.view("int16")).cuda()
     d_if = torch.from_numpy(ifidx.view("int32")).cuda()
@@ -44,8 +47,8 @@ def run_br(reps, n=1 << 20):
 
 def main():
     keysel = sys.argv[1] if len(sys.argv) > 1 else "zero"
-    if keysel == "br":
-        return run_br(int(sys.argv[2]) if len(sys.argv) > 2 else 10)
+    if keysel in ("br", "br1t"):
+        return run_br(int(sys.argv[2]) if len(sys.argv) > 2 else 10, one=keysel == "br1t")
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     sizes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1048576,16777216").split(",")]
     svc = len(sys.argv) > 4 and sys.argv[4] in ("svc", "svcrun")

@@ -29,7 +29,7 @@ if [[ $SVC == bat ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576,16777216 k_verify_batches 10
 elif [[ $SVC == svc ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576,16777216 k_verify_service 10
-elif [[ $KS == br ]]; then
+elif [[ $KS == br* ]]; then
     python3 scripts/pmc_summary.py $OUT 1048576 k_br_process
 else
     python3 scripts/pmc_summary.py $OUT

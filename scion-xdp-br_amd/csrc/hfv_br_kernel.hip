@@ -13,10 +13,11 @@
 // bpf_fib_lookup is replaced by the static next-hop table of the installed hfv_br_config.
 //
 // Mapping: one lane per frame, a persistent grid with one block per CU (1024 threads = 16 waves).
-// Each block builds the AES round tables in LDS (T0/T1, 4 lane replicas, 8 KiB: AES is a small
+// Each block builds the AES round tables in LDS (T0/T1, 8 lane replicas, 16 KiB: AES is a small
 // part of the router's work, so LDS goes to header rows),
-// and stages the router tables (~6.5 KiB), its verdict counters (11 KiB) and, in the staged
-// variant, the first 128 bytes of each frame of its waves' tiles.  The rewrite patches the
+// and stages the router tables (~6.5 KiB), its verdict counters (5.5 KiB of 32-bit words) and, in
+// the staged variant, the first 128 bytes of each frame of its waves' tiles (a frame whose header
+// runs past them also gets bytes 128-135 in registers, HFV_BR_EXT).  The rewrite patches the
 // staged rows, and only the 16-byte chunks it touched go back to HBM; payload bytes are never
 // read.  At most one hop field is checked per frame (ingress from a neighbour AS or
 // egress of a packet from the own AS), with the record-verify kernel's AES code (slot-0 key
